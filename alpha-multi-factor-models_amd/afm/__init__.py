@@ -1,0 +1,18 @@
+"""afm -- MI355X-native engine for the factor-research hot path of
+Yuliang-Eliott/Alpha-Multi-factor-models.
+
+Drop-in Python surface (same names, arguments and results as the reference):
+
+* ``compute_factors(data)``                      -- No-talib.py:1-93
+* ``AlphaSignalAnalyzer(df, name, prices).run()`` -- KKT Yuliang Jiang.py:280-375
+* ``LinearRegression().fit/predict``              -- KKT:582-598 (pooled OLS)
+* ``PortfolioManager(...)``                       -- KKT:795-970
+
+All compute runs in hand-written HIP kernels (libafm.so, C-ABI in include/afm.h); there is no
+CPU fallback.
+"""
+from .factors import FACTOR_NAMES, compute_factors, factor_panel  # noqa: F401
+from .grid import PanelGrid, pack_bits, unpack_bits  # noqa: F401
+
+__all__ = ["compute_factors", "factor_panel", "FACTOR_NAMES", "PanelGrid", "pack_bits",
+           "unpack_bits"]

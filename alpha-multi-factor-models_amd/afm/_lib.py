@@ -1,0 +1,103 @@
+"""ctypes binding of libafm.so (the C-ABI declared in include/afm.h).
+
+The product path has no CPU fallback: if the library is missing or no GPU is visible, every
+call raises.  ``make -C alpha-multi-factor-models_amd`` (or ``__graft_entry__.build()``) builds
+the library in-tree.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libafm.so")
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+DBL = ctypes.c_double
+
+# name -> (restype, argtypes); kept in sync with include/afm.h (tests/test_abi.py checks it)
+SIGNATURES = {
+    "afm_ctx_create": (I32, [I32, ctypes.POINTER(P)]),
+    "afm_ctx_set_stream": (I32, [P, P]),
+    "afm_ctx_destroy": (I32, [P]),
+    "afm_last_error": (ctypes.c_char_p, []),
+    "afm_version": (I32, []),
+    "afm_factor_name": (ctypes.c_char_p, [I32]),
+    "afm_factors_f64": (I32, [P, I64, I64, I64, P, P, P, P, P, P, P]),
+}
+
+
+class AfmError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(f"{LIB_PATH} is not built: run `make -C "
+                                      f"{os.path.dirname(HERE)}` (hipcc, gfx950)")
+                L = ctypes.CDLL(LIB_PATH)
+                for name, (res, args) in SIGNATURES.items():
+                    f = getattr(L, name)
+                    f.restype = res
+                    f.argtypes = args
+                _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().afm_last_error().decode(errors="replace")
+        raise AfmError(f"{what or 'afm'} failed ({rc}): {msg}")
+
+
+class Context:
+    """One afm_ctx per device; calls are issued on torch's current stream of that device."""
+
+    _by_device: dict = {}
+
+    def __init__(self, device: int):
+        self.device = device
+        h = P()
+        check(lib().afm_ctx_create(device, ctypes.byref(h)), "afm_ctx_create")
+        self.handle = h
+
+    @classmethod
+    def get(cls, device: int | None = None) -> "Context":
+        import torch
+        if not torch.cuda.is_available():
+            raise AfmError("no GPU visible: the afm engine runs on MI355X only (no CPU fallback)")
+        if device is None:
+            device = torch.cuda.current_device()
+        ctx = cls._by_device.get(device)
+        if ctx is None:
+            ctx = cls._by_device[device] = Context(device)
+        return ctx
+
+    def bind_stream(self):
+        import torch
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        check(lib().afm_ctx_set_stream(self.handle, P(s)), "afm_ctx_set_stream")
+        return self.handle
+
+
+def ptr(t) -> P:
+    """Device pointer of a contiguous torch tensor."""
+    if not t.is_contiguous():
+        raise AfmError("tensor must be contiguous")
+    return P(t.data_ptr())
+
+
+def factor_names() -> list:
+    L = lib()
+    return [L.afm_factor_name(i).decode() for i in range(98)]

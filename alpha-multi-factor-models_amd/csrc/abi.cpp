@@ -1,0 +1,70 @@
+// Context, error and metadata entry points of the C-ABI (include/afm.h).
+#include "afm_internal.h"
+
+static thread_local std::string g_last_error;
+
+void afm_set_error(const std::string& msg) { g_last_error = msg; }
+
+extern "C" {
+
+const char* afm_last_error(void) { return g_last_error.c_str(); }
+
+int afm_version(void) { return 1; }
+
+int afm_ctx_create(int device, afm_ctx** out) {
+    AFM_CHECK_ARG(out != nullptr, "out is null");
+    int n = 0;
+    AFM_HIP(hipGetDeviceCount(&n));
+    AFM_CHECK_ARG(device >= 0 && device < n, "device ordinal out of range");
+    AFM_HIP(hipSetDevice(device));
+    afm_ctx* c = new afm_ctx();
+    c->device = device;
+    *out = c;
+    return AFM_OK;
+}
+
+int afm_ctx_set_stream(afm_ctx* ctx, void* stream) {
+    AFM_CTX(ctx);
+    ctx->stream = reinterpret_cast<hipStream_t>(stream);
+    return AFM_OK;
+}
+
+int afm_ctx_destroy(afm_ctx* ctx) {
+    if (!ctx || ctx->magic != 0x61666d31) {
+        afm_set_error("afm_ctx_destroy: invalid afm_ctx");
+        return AFM_E_STATE;
+    }
+    ctx->magic = 0;
+    delete ctx;
+    return AFM_OK;
+}
+
+static const char* kFactorNames[AFM_N_FACTORS] = {
+    "SMA_6", "SMA_10", "SMA_14", "SMA_18", "SMA_22", "SMA_26", "SMA_30", "SMA_34", "SMA_38",
+    "SMA_42", "SMA_46", "SMA_50",
+    "EMA_6", "EMA_10", "EMA_14", "EMA_18", "EMA_22", "EMA_26", "EMA_30", "EMA_34", "EMA_38",
+    "EMA_42", "EMA_46", "EMA_50",
+    "VWMA_6", "VWMA_10", "VWMA_14", "VWMA_18", "VWMA_22", "VWMA_26", "VWMA_30", "VWMA_34",
+    "VWMA_38", "VWMA_42", "VWMA_46", "VWMA_50",
+    "BBANDS_upper_14", "BBANDS_lower_14", "BBANDS_upper_20", "BBANDS_lower_20",
+    "BBANDS_upper_26", "BBANDS_lower_26", "BBANDS_upper_32", "BBANDS_lower_32",
+    "BBANDS_upper_38", "BBANDS_lower_38", "BBANDS_upper_44", "BBANDS_lower_44",
+    "BBANDS_upper_50", "BBANDS_lower_50", "BBANDS_upper_56", "BBANDS_lower_56",
+    "MOM_14", "MOM_20", "MOM_26", "MOM_32", "MOM_38", "MOM_44", "MOM_50", "MOM_56",
+    "ACCEL_14", "ACCEL_20", "ACCEL_26", "ACCEL_32", "ACCEL_38", "ACCEL_44", "ACCEL_50", "ACCEL_56",
+    "ROCR_14", "ROCR_20", "ROCR_26", "ROCR_32", "ROCR_38", "ROCR_44", "ROCR_50", "ROCR_56",
+    "MACD_12_18", "MACD_12_24", "MACD_12_30",
+    "RSI_8", "RSI_14", "RSI_20",
+    "PVT", "OBV", "PSY",
+    "sd_3", "sd_5", "sd_15", "sd5_15",
+    "volsd_3", "volsd_5", "volsd_15", "volsd5_15",
+    "vol_change", "corr_5", "corr_15",
+    "target", "tmr_ret1d",
+};
+
+const char* afm_factor_name(int i) {
+    if (i < 0 || i >= AFM_N_FACTORS) return nullptr;
+    return kFactorNames[i];
+}
+
+}  // extern "C"

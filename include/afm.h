@@ -1,0 +1,63 @@
+/* afm.h -- C-ABI of the MI355X engine for the factor-research hot path of
+ * Yuliang-Eliott/Alpha-Multi-factor-models.
+ *
+ * The reference has no FFI: its boundary is a set of pandas-in/pandas-out Python signatures
+ * (SURVEY.md §8(b)).  Each entry point below replaces the compute behind one of them; the Python
+ * mirror in alpha-multi-factor-models_amd/afm/ (ctypes) rebuilds the reference's DataFrames
+ * around these calls, and INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *  - Every function returns 0 on success, a negative AFM_E* code on failure; the message of
+ *    the last failure on the calling thread is afm_last_error().  Nothing throws across the ABI.
+ *  - Buffers are caller-owned DEVICE pointers (hipMalloc / torch CUDA tensors) unless a
+ *    parameter says "host".  The library never frees caller memory and keeps no global state
+ *    besides the per-thread error string; work runs on the context's stream, asynchronously.
+ *  - Panels are CALENDAR GRIDS: row-major [T][lda] float64 (date-major, asset-minor), lda a
+ *    multiple of 64 >= A.  Presence of an asset-day is a bit mask: word [c][a] (uint64) holds
+ *    days 64c..64c+63 of asset a in bits 0..63.  Windows are positional over each asset's
+ *    present days, exactly as the reference's per-security pandas frames (No-talib.py:5-6).
+ *  - Arithmetic is IEEE fp64 without FMA contraction, reproducing pandas 2.3.3 bit-for-bit.
+ */
+#ifndef AFM_H
+#define AFM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AFM_OK 0
+#define AFM_E_ARG (-1)      /* invalid argument (shape, null pointer, alignment) */
+#define AFM_E_HIP (-2)      /* HIP runtime error */
+#define AFM_E_STATE (-3)    /* misuse (destroyed context, ...) */
+
+typedef struct afm_ctx afm_ctx;
+
+#define AFM_N_FACTORS 98    /* No-talib.py output columns: 96 factors + target + tmr_ret1d */
+
+/* ---- context --------------------------------------------------------------------------- */
+int afm_ctx_create(int device, afm_ctx** out);
+/* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = default stream */
+int afm_ctx_set_stream(afm_ctx* ctx, void* stream);
+int afm_ctx_destroy(afm_ctx* ctx);
+const char* afm_last_error(void);
+int afm_version(void);
+/* Name of factor column i (0 <= i < AFM_N_FACTORS), No-talib.py creation order; host string. */
+const char* afm_factor_name(int i);
+
+/* ---- I0-I16: factor panel -- replaces compute_factors(data) (No-talib.py:1-93) -----------
+ * Inputs [T][lda]: close_price, volume, ret1d, excess_ret1d; valid_bits [ceil(T/64)][lda].
+ * out: [AFM_N_FACTORS][T][lda]; cells of absent asset-days are left untouched.
+ * nanfree_bits [ceil(T/64)][lda]: present AND all 96 factor columns non-NaN (target/tmr_ret1d
+ * excluded: their NaN-ness is read from their planes), i.e. the dropna() row mask of
+ * No-talib.py:33 before the pass-through and label columns are considered. */
+int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
+                    const double* close, const double* volume, const double* ret1d,
+                    const double* excess, const uint64_t* valid_bits,
+                    double* out, uint64_t* nanfree_bits);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AFM_H */

@@ -1,0 +1,70 @@
+"""GPU parity of the factor panel (afm_factors_f64) -- bit-exact against the oracle and the
+reference's own outputs (tests/golden/factors_*.npz)."""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from helpers import mismatch_report, oracle_panel, same
+
+pytestmark = pytest.mark.gpu
+
+
+def frame_from(g):
+    return pd.DataFrame({
+        "data_date": g["in_date"].astype("datetime64[ns]"), "security_id": g["in_id"],
+        "close_price": g["in_close"], "volume": g["in_volume"], "ret1d": g["in_ret1d"],
+        "excess_ret1d": g["in_excess"], "group_id": g["in_group"],
+        "in_trading_universe": np.where(g["in_tradable"], "Y", "N")})
+
+
+@pytest.mark.parametrize("name", ["edge", "scales", "pipeline"])
+def test_compute_factors_matches_reference(golden_dir, name):
+    import afm
+    g = np.load(os.path.join(golden_dir, f"factors_{name}.npz"))
+    out = afm.compute_factors(frame_from(g))
+    assert np.array_equal(out.index.values, g["out_index"])
+    assert np.array_equal(out["security_id"].values, g["out_id"])
+    cols = list(g["out_cols"])
+    got = out[cols].to_numpy(np.float64)
+    assert same(got, g["out"]), mismatch_report(got, g["out"], cols)
+
+
+@pytest.mark.parametrize("A,T,seed,kw", [
+    (70, 333, 1, dict(edge_cases=True, hole_frac=0.02, listing_frac=0.3)),
+    (300, 900, 2, dict(hole_frac=0.002)),
+    (64, 64, 3, dict(hole_frac=0.05)),
+    (5, 130, 4, dict(edge_cases=True)),
+])
+def test_factor_grid_vs_oracle(A, T, seed, kw):
+    import torch
+    import afm
+    from afm.synthetic import make_panel
+    p = make_panel(A, T, seed=seed, **kw)
+    grid = afm.PanelGrid.from_panel(p)
+    out, nanfree = afm.factor_panel(grid)
+    torch.cuda.synchronize()
+    tt, aa, ref = oracle_panel(p)
+    got = out[:, torch.from_numpy(tt).cuda(), torch.from_numpy(aa).cuda()].T.cpu().numpy()
+    assert same(got, ref), mismatch_report(got, ref, afm.FACTOR_NAMES)
+    # absent cells untouched (still the NaN fill), nanfree = present & no NaN in 96 factors
+    o = out.cpu().numpy()
+    assert np.isnan(o[:, ~p.valid]).all()
+    nf = afm.unpack_bits(nanfree, T).cpu().numpy()
+    exp = np.zeros_like(p.valid)
+    exp[tt, aa] = ~np.isnan(ref[:, :96]).any(axis=1)
+    assert np.array_equal(nf, exp)
+
+
+def test_factor_kernel_rejects_bad_shapes():
+    import torch
+    import afm
+    from afm import _lib
+    from afm.synthetic import make_panel
+    p = make_panel(10, 100, seed=0)
+    grid = afm.PanelGrid.from_panel(p)
+    ctx = _lib.Context.get()
+    rc = _lib.lib().afm_factors_f64(ctx.bind_stream(), 100, 10, 60, *([None] * 7))
+    assert rc != 0 and b"lda" in _lib.lib().afm_last_error()
+    torch.cuda.synchronize()
