@@ -13,6 +13,8 @@ CPU fallback.
 """
 from .factors import FACTOR_NAMES, compute_factors, factor_panel  # noqa: F401
 from .grid import PanelGrid, pack_bits, unpack_bits  # noqa: F401
+from . import regression  # noqa: F401
+from .regression import LinearRegression, cross_sectional_ols  # noqa: F401
 
 __all__ = ["compute_factors", "factor_panel", "FACTOR_NAMES", "PanelGrid", "pack_bits",
            "unpack_bits"]

@@ -1,0 +1,457 @@
+// Cross-sectional regression: per-segment shifted Gram matrices on fp64
+// MFMA, batched scaled-Cholesky OLS solves, the pooled (train+valid) OLS as an exact Chan
+// combination of the per-segment moments, Fama-MacBeth statistics and predictions.
+//
+// A "segment" is the set of rows reduced into one Gram: one DATE of a calendar-grid panel
+// (rows = the assets present that day, read straight from the factor planes), or one block of
+// rows of a long design matrix (the LinearRegression drop-in, KKT:582-590).
+//
+// Gram kernel (one workgroup = 4 waves per segment):
+//   Z = [1, x_1 .. x_p, y] over the segment's usable rows (mask bit set and every value finite),
+//   shifted by the first usable row s (Z - s keeps the moments well conditioned; column 0 is
+//   not shifted), G' = sum_rows (z - s)(z - s)^T.  Rows are staged 64 at a time through an LDS
+//   tile [feature][row] (row stride 66 doubles -> conflict-free fragment reads) and reduced with
+//   v_mfma_f64_16x16x4_f64 over the upper-triangle 16x16 tile pairs; waves split tile pairs
+//   (wide designs) and/or rows (narrow designs), partial sums are combined in a fixed order, so
+//   results are deterministic.
+// Algorithmic work per segment: rows * (p+2)(p+3) flops over 8(p+1) B per row.
+#include "afm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace afm {
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64;
+
+constexpr int kMaxTiles = 7;          // p + 2 <= 112
+constexpr int kMaxF = kMaxTiles * 16;
+constexpr int kRS = 66;               // LDS tile row stride (doubles)
+constexpr int kRows = 64;             // rows staged per tile
+constexpr int kThreads = 256;
+
+struct GramArgs {
+    const double* base;      // planes / columns
+    int64_t col_stride;      // elements between two columns
+    int64_t seg_stride;      // elements between the first rows of two consecutive segments
+    int64_t seg_rows;        // rows per segment
+    int64_t row_limit;       // long mode: total rows (rows >= limit are masked); grid: -1
+    const int32_t* cols;     // [p] column indices of the regressors
+    int32_t ycol;            // column index of the regressand
+    int p;
+    const uint64_t* bits;    // grid mode: [ceil(T/64)][seg_stride] presence words; may be null
+    int64_t seg0;            // first segment (date) index
+    double* gram;            // [nseg][p2][p2]
+    double* shift;           // [nseg][p2]
+};
+
+__device__ __forceinline__ int pair_I(int q, int nt) {
+    int I = 0;
+    while (q >= nt - I) { q -= nt - I; ++I; }
+    return I;
+}
+__device__ __forceinline__ int pair_J(int q, int nt) {
+    int I = 0;
+    while (q >= nt - I) { q -= nt - I; ++I; }
+    return I + q;
+}
+
+__global__ __launch_bounds__(kThreads) void gram_kernel(GramArgs g) {
+    __shared__ double tile[kMaxF][kRS];
+    __shared__ double sh[kMaxF];
+    __shared__ int rowok[kRows];
+    __shared__ int flags[2];               // [0] shift set, [1] tile has a usable row
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int p = g.p, p2 = p + 2;
+    const int nt = (p2 + 15) / 16;
+    const int npairs = nt * (nt + 1) / 2;
+    // split 4 waves over tile pairs (WP) x row k-steps (WK)
+    const int WP = npairs >= 8 ? 4 : (npairs >= 3 ? 2 : 1);
+    const int WK = 4 / WP;
+    const int wp = wave % WP, wk = wave / WP;
+    const int64_t seg = g.seg0 + blockIdx.x;
+    const int64_t rowbase = seg * g.seg_stride;
+
+    for (int i = tid; i < kMaxF * kRS; i += kThreads) (&tile[0][0])[i] = 0.0;
+    if (tid < kMaxF) sh[tid] = 0.0;
+    if (tid == 0) flags[0] = 0;
+    d4 acc[kMaxTiles];
+#pragma unroll
+    for (int q = 0; q < kMaxTiles; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    __syncthreads();
+
+    for (int64_t r0 = 0; r0 < g.seg_rows; r0 += kRows) {
+        // ---- stage rows r0..r0+63 of features 1..p+1 ----
+        if (tid < kRows) {
+            int64_t r = r0 + tid;
+            bool ok = r < g.seg_rows;
+            if (ok && g.row_limit >= 0) ok = rowbase + r < g.row_limit;
+            if (ok && g.bits) {
+                u64 w = g.bits[(seg >> 6) * g.seg_stride + r];
+                ok = (w >> (seg & 63)) & 1ull;
+            }
+            rowok[tid] = ok ? 1 : 0;
+        }
+        __syncthreads();
+        for (int i = tid; i < (p + 1) * kRows; i += kThreads) {
+            int f = 1 + i / kRows, a = i % kRows;
+            double x = 0.0;
+            if (rowok[a]) {
+                int c = f <= p ? g.cols[f - 1] : g.ycol;
+                x = g.base[(int64_t)c * g.col_stride + rowbase + r0 + a];
+                if (!__builtin_isfinite(x)) rowok[a] = 0;   // benign race: every writer stores 0
+            }
+            tile[f][a] = x;
+        }
+        __syncthreads();
+        if (wave == 0) {
+            u64 m = __ballot(rowok[lane] != 0);
+            if (lane == 0) flags[1] = m != 0ull;
+            if (m != 0ull && flags[0] == 0) {
+                int a0 = __builtin_ctzll(m);
+                for (int f = 1 + lane; f < p2; f += 64) sh[f] = tile[f][a0];
+                if (lane == 0) flags[0] = 1;
+            }
+        }
+        __syncthreads();
+        if (!flags[1]) continue;                   // uniform: nothing usable in this tile
+        for (int i = tid; i < p2 * kRows; i += kThreads) {
+            int f = i / kRows, a = i % kRows;
+            double v = 0.0;
+            if (rowok[a]) v = (f == 0) ? 1.0 : tile[f][a] - sh[f];
+            tile[f][a] = v;
+        }
+        __syncthreads();
+        // ---- MFMA: acc[pair] += Z[:, I]^T Z[:, J] over this wave's k-steps ----
+        const int fi = lane & 15, kk = lane >> 4;
+        for (int ks = wk; ks < kRows / 4; ks += WK) {
+            const int a = ks * 4 + kk;
+#pragma unroll
+            for (int q = 0; q < kMaxTiles; ++q) {
+                const int pq = wp + q * WP;
+                if (pq < npairs) {
+                    const int I = pair_I(pq, nt), J = pair_J(pq, nt);
+                    double va = tile[I * 16 + fi][a];
+                    double vb = tile[J * 16 + fi][a];
+                    acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc[q], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- combine the WK row-groups in a fixed order, write G' (full symmetric) ----
+    double* out = g.gram + (int64_t)blockIdx.x * p2 * p2;
+    double* red = &tile[0][0];               // reuse: [WK][kMaxTiles][64 lanes][4]
+    const int per = kMaxTiles * 64 * 4;
+    if (WK > 1) {
+        for (int q = 0; q < kMaxTiles; ++q)
+            for (int r = 0; r < 4; ++r) red[wk * per + (q * 64 + lane) * 4 + r] = acc[q][r];
+        __syncthreads();
+    }
+    if (wk == 0) {
+        for (int q = 0; q < kMaxTiles; ++q) {
+            const int pq = wp + q * WP;
+            if (pq >= npairs) continue;
+            const int I = pair_I(pq, nt), J = pair_J(pq, nt);
+            for (int r = 0; r < 4; ++r) {
+                double v = acc[q][r];
+                for (int k = 1; k < WK; ++k) v += red[k * per + (q * 64 + lane) * 4 + r];
+                const int row = I * 16 + (lane >> 4) + 4 * r;   // f64 MFMA C/D layout
+                const int col = J * 16 + (lane & 15);
+                if (row < p2 && col < p2) {
+                    out[row * p2 + col] = v;
+                    out[col * p2 + row] = v;
+                }
+            }
+        }
+    }
+    if (tid < p2) g.shift[(int64_t)blockIdx.x * p2 + tid] = sh[tid];
+}
+
+// ---- per-segment OLS from the shifted Gram -------------------------------------------------
+// C = G'[1:,1:] - G'[0,1:] G'[0,1:]^T / n (centered moments of [x, y]); scale to unit diagonal,
+// Cholesky with a relative pivot threshold (a pivot below tol drops the regressor: beta = 0),
+// beta = D b, intercept = ybar - xbar . beta.  One workgroup per segment, matrices in LDS.
+struct SolveArgs {
+    const double* gram;      // [nseg][p2][p2]
+    const double* shift;     // [nseg][p2]
+    int p;
+    double tol;
+    double* beta;            // [nseg][p+1]: intercept, beta_1..p
+    double* nobs;            // [nseg]
+    int32_t* rank;           // [nseg]
+};
+
+constexpr int kMaxP = kMaxF - 2;
+
+__global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
+    __shared__ double M[kMaxP][kMaxP + 1];
+    __shared__ double rhs[kMaxP];
+    __shared__ double dsc[kMaxP];
+    __shared__ double mean[kMaxP + 2];
+    __shared__ int drop[kMaxP];
+    __shared__ double piv;
+    const int tid = threadIdx.x;
+    const int p = s.p, p2 = p + 2;
+    const double* G = s.gram + (int64_t)blockIdx.x * p2 * p2;
+    const double* sf = s.shift + (int64_t)blockIdx.x * p2;
+    const double n = G[0];
+    double* beta = s.beta + (int64_t)blockIdx.x * (p + 1);
+    if (tid == 0) s.nobs[blockIdx.x] = n;
+    if (!(n > (double)p)) {                          // under-determined segment
+        for (int j = tid; j <= p; j += kThreads) beta[j] = __builtin_nan("");
+        if (tid == 0) s.rank[blockIdx.x] = 0;
+        return;
+    }
+    for (int j = tid; j < p2; j += kThreads) mean[j] = (j == 0) ? 1.0 : G[j] / n;   // shifted
+    __syncthreads();
+    for (int i = tid; i < p * p; i += kThreads) {
+        int r = i / p, c = i % p;
+        M[r][c] = G[(r + 1) * p2 + (c + 1)] - G[r + 1] * G[c + 1] / n;
+    }
+    for (int r = tid; r < p; r += kThreads) rhs[r] = G[(r + 1) * p2 + (p + 1)] - G[r + 1] * G[p + 1] / n;
+    __syncthreads();
+    for (int r = tid; r < p; r += kThreads) {
+        double d = M[r][r];
+        dsc[r] = d > 0 ? 1.0 / __builtin_sqrt(d) : 0.0;
+        drop[r] = !(d > 0);
+    }
+    __syncthreads();
+    for (int i = tid; i < p * p; i += kThreads) {
+        int r = i / p, c = i % p;
+        M[r][c] = M[r][c] * dsc[r] * dsc[c];
+    }
+    for (int r = tid; r < p; r += kThreads) rhs[r] = rhs[r] * dsc[r];
+    __syncthreads();
+    // right-looking Cholesky (lower), thresholded
+    for (int k = 0; k < p; ++k) {
+        if (tid == 0) {
+            double d = M[k][k];
+            if (drop[k] || !(d > s.tol)) {
+                drop[k] = 1;
+                piv = 0.0;
+            } else {
+                piv = __builtin_sqrt(d);
+            }
+        }
+        __syncthreads();
+        const double pk = piv;
+        if (pk == 0.0) {
+            for (int i = tid; i < p; i += kThreads) { M[i][k] = 0.0; M[k][i] = 0.0; }
+            __syncthreads();
+            continue;
+        }
+        for (int i = k + tid; i < p; i += kThreads) M[i][k] = (i == k) ? pk : M[i][k] / pk;
+        __syncthreads();
+        const int m = p - k - 1;
+        for (int e = tid; e < m * m; e += kThreads) {
+            int i = k + 1 + e / m, j = k + 1 + e % m;
+            if (j <= i) M[i][j] = M[i][j] - M[i][k] * M[j][k];
+        }
+        __syncthreads();
+    }
+    // forward / back substitution (sequential in k; every wave takes part in the barriers)
+    for (int k = 0; k < p; ++k) {
+        if (tid == 0) rhs[k] = drop[k] ? 0.0 : rhs[k] / M[k][k];
+        __syncthreads();
+        const double v = rhs[k];
+        for (int i = k + 1 + tid; i < p; i += kThreads) rhs[i] = rhs[i] - M[i][k] * v;
+        __syncthreads();
+    }
+    for (int k = p - 1; k >= 0; --k) {
+        if (tid == 0) rhs[k] = drop[k] ? 0.0 : rhs[k] / M[k][k];
+        __syncthreads();
+        const double v = rhs[k];
+        for (int i = tid; i < k; i += kThreads) rhs[i] = rhs[i] - M[k][i] * v;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        double icpt = sf[p + 1] + mean[p + 1];           // ybar
+        int rk = 0;
+        for (int j = 0; j < p; ++j) {
+            double b = rhs[j] * dsc[j];
+            beta[1 + j] = b;
+            icpt = icpt - (sf[1 + j] + mean[1 + j]) * b;
+            rk += drop[j] ? 0 : 1;
+        }
+        beta[0] = icpt;
+        s.rank[blockIdx.x] = rk;
+    }
+}
+
+// ---- exact (Chan) combination of per-segment shifted moments over [s0, s1) -----------------
+// out: centered Gram of the union in the same "shifted" representation (shift = 0, column 0
+// carries n and the sums) so ols_solve_kernel solves the pooled problem unchanged.
+__global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, const double* shift,
+                                                        int p2, int64_t nseg, double* out_gram,
+                                                        double* out_shift) {
+    __shared__ double mu[kMaxF];       // running mean (unshifted)
+    __shared__ double dl[kMaxF];       // delta of the segment mean vs the running mean
+    __shared__ double ntot;
+    __shared__ double fac;
+    const int tid = threadIdx.x;
+    const int q2 = p2 * p2;
+    constexpr int per = 40;            // this thread's centered entries (up to 40 x 256 = 10240)
+    double C[per];
+#pragma unroll
+    for (int k = 0; k < per; ++k) C[k] = 0.0;
+    if (tid < p2) mu[tid] = 0.0;
+    if (tid == 0) ntot = 0.0;
+    __syncthreads();
+    for (int64_t sg = 0; sg < nseg; ++sg) {
+        const double* G = gram + sg * q2;
+        const double* S = shift + sg * p2;
+        const double nb = G[0];
+        if (!(nb > 0)) continue;
+        if (tid < p2 && tid > 0) {
+            double mb = S[tid] + G[tid] / nb;        // segment mean
+            dl[tid] = mb - mu[tid];
+        }
+        if (tid == 0) {
+            double na = ntot;
+            fac = na * nb / (na + nb);
+            ntot = na + nb;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < per; ++k) {
+            int e = tid + k * kThreads;
+            if (e < q2) {
+                int r = e / p2, c = e % p2;
+                if (r > 0 && c > 0) {
+                    double cb = G[r * p2 + c] - G[r] * G[c] / nb;   // segment centered
+                    C[k] = C[k] + cb + dl[r] * dl[c] * fac;
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < p2 && tid > 0) mu[tid] = mu[tid] + dl[tid] * (nb / ntot);
+        __syncthreads();
+    }
+    // emit as a Gram with shift = mu: G'[0][0] = n, G'[0][j] = 0 (centered), G'[i][j] = C
+#pragma unroll
+    for (int k = 0; k < per; ++k) {
+        int e = tid + k * kThreads;
+        if (e < q2) {
+            int r = e / p2, c = e % p2;
+            double v;
+            if (r == 0 && c == 0) v = ntot;
+            else if (r == 0 || c == 0) v = 0.0;
+            else v = C[k];
+            out_gram[e] = v;
+        }
+    }
+    if (tid < p2) out_shift[tid] = (tid == 0) ? 0.0 : mu[tid];
+}
+
+// ---- predictions: pred[t][a] = beta0 + sum_j beta_j x_j (grid rows with a set mask bit) ------
+__global__ __launch_bounds__(256) void predict_kernel(const double* base, int64_t col_stride,
+                                                      int64_t lda, int64_t t0, int64_t nt,
+                                                      const int32_t* cols, int p,
+                                                      const double* beta, int64_t beta_stride,
+                                                      const uint64_t* bits, double* pred) {
+    const int64_t a = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int64_t t = t0 + (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (t >= t0 + nt) return;
+    const double* b = beta + (t - t0) * beta_stride;
+    u64 w = bits[(t >> 6) * lda + a];
+    double v = __builtin_nan("");
+    if ((w >> (t & 63)) & 1ull) {
+        double s = b[0];
+        for (int j = 0; j < p; ++j) s = s + b[1 + j] * base[(int64_t)cols[j] * col_stride + t * lda + a];
+        v = s;
+    }
+    pred[t * lda + a] = v;
+}
+
+// ---- Fama-MacBeth: mean_t beta_t and t = mean / (std / sqrt(T)) over segments with rank > 0 --
+__global__ void fama_macbeth_kernel(const double* beta, const int32_t* rank, int64_t nseg, int k,
+                                    double* mean_out, double* t_out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= k) return;
+    double n = 0, m = 0, m2 = 0;
+    for (int64_t s = 0; s < nseg; ++s) {
+        if (rank[s] <= 0) continue;
+        double x = beta[s * k + j];
+        n += 1;
+        double d = x - m;
+        m += d / n;
+        m2 += d * (x - m);
+    }
+    double sd = n > 1 ? __builtin_sqrt(m2 / (n - 1)) : __builtin_nan("");
+    mean_out[j] = n > 0 ? m : __builtin_nan("");
+    t_out[j] = m / (sd / __builtin_sqrt(n));
+}
+
+}  // namespace
+}  // namespace afm
+
+using namespace afm;
+
+extern "C" int afm_xs_gram_f64(afm_ctx* ctx, const double* base, int64_t col_stride,
+                               int64_t seg_stride, int64_t seg_rows, int64_t row_limit,
+                               const int32_t* cols, int p, int ycol, const uint64_t* bits,
+                               int64_t seg0, int64_t nseg, double* gram, double* shift) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(p >= 1 && p + 2 <= kMaxF, "need 1 <= p <= 110");
+    AFM_CHECK_ARG(base && cols && gram && shift, "null buffer");
+    AFM_CHECK_ARG(nseg >= 0 && seg0 >= 0 && seg_rows > 0, "bad segment range");
+    AFM_CHECK_ARG(!bits || seg_stride % 64 == 0, "grid mode needs seg_stride (lda) % 64 == 0");
+    if (nseg == 0) return AFM_OK;
+    GramArgs g{base, col_stride, seg_stride, seg_rows, row_limit, cols, ycol, p, bits, seg0, gram,
+               shift};
+    hipLaunchKernelGGL(gram_kernel, dim3((unsigned)nseg), dim3(kThreads), 0, ctx->stream, g);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
+                                 int64_t nseg, double tol, double* beta, double* nobs,
+                                 int32_t* rank) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(p >= 1 && p <= kMaxP, "need 1 <= p <= 110");
+    AFM_CHECK_ARG(gram && shift && beta && nobs && rank, "null buffer");
+    if (nseg <= 0) return AFM_OK;
+    SolveArgs s{gram, shift, p, tol, beta, nobs, rank};
+    hipLaunchKernelGGL(ols_solve_kernel, dim3((unsigned)nseg), dim3(kThreads), 0, ctx->stream, s);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
+                                    int64_t nseg, double* out_gram, double* out_shift) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(p >= 1 && (p + 2) * (p + 2) <= 40 * kThreads, "p too large for pooling");
+    AFM_CHECK_ARG(gram && shift && out_gram && out_shift, "null buffer");
+    hipLaunchKernelGGL(pool_kernel, dim3(1), dim3(kThreads), 0, ctx->stream, gram, shift, p + 2,
+                       nseg, out_gram, out_shift);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_predict_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
+                               int64_t t0, int64_t nt, const int32_t* cols, int p,
+                               const double* beta, int64_t beta_stride, const uint64_t* bits,
+                               double* pred) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(base && cols && beta && bits && pred, "null buffer");
+    AFM_CHECK_ARG(lda % 64 == 0 && nt >= 0 && t0 >= 0, "bad shape");
+    if (nt == 0) return AFM_OK;
+    dim3 grid((unsigned)(lda / 64), (unsigned)((nt + 3) / 4));
+    hipLaunchKernelGGL(predict_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride, lda, t0,
+                       nt, cols, p, beta, beta_stride, bits, pred);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_fama_macbeth_f64(afm_ctx* ctx, const double* beta, const int32_t* rank,
+                                    int64_t nseg, int k, double* mean_out, double* t_out) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(beta && rank && mean_out && t_out && k > 0, "bad args");
+    hipLaunchKernelGGL(fama_macbeth_kernel, dim3((k + 63) / 64), dim3(64), 0, ctx->stream, beta,
+                       rank, nseg, k, mean_out, t_out);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}

@@ -57,6 +57,35 @@ int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                     const double* excess, const uint64_t* valid_bits,
                     double* out, uint64_t* nanfree_bits);
 
+/* ---- R1: cross-sectional regression ---------------------------------------------------------
+ * Segmented shifted Gram on fp64 MFMA.  Segment t (t = seg0 .. seg0+nseg-1) is the rows
+ * [t*seg_stride, t*seg_stride + seg_rows) of every column; column c starts at base + c*col_stride.
+ * Grid mode (bits != NULL): seg_stride = lda, seg_rows = A, segment = date t, a row is used when
+ * bit (t & 63) of bits[(t >> 6) * lda + row] is set.  Long mode (bits == NULL): rows at or past
+ * row_limit (>= 0) are masked.  Rows with any non-finite value among [x_cols.., y] are skipped.
+ * Z = [1, x_cols[0..p), y]; gram[s] = sum (z - shift[s]) (z - shift[s])^T  ((p+2)^2 entries),
+ * shift[s] = the first usable row (column 0 unshifted).  1 <= p <= 110.  cols: DEVICE int32[p]. */
+int afm_xs_gram_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t seg_stride,
+                    int64_t seg_rows, int64_t row_limit, const int32_t* cols, int p, int ycol,
+                    const uint64_t* bits, int64_t seg0, int64_t nseg, double* gram, double* shift);
+/* OLS with intercept per segment from (gram, shift): beta[s] = [intercept, b_1..b_p].  Scaled
+ * (unit-diagonal) Cholesky of the centered normal equations; a regressor whose pivot falls below
+ * tol is dropped (b = 0) -- rank[s] counts the kept ones.  Segments with n <= p get NaN. */
+int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double* shift, int p, int64_t nseg,
+                      double tol, double* beta, double* nobs, int32_t* rank);
+/* Exact (Chan) combination of nseg per-segment moments into one (gram, shift) -- the pooled OLS
+ * of KKT:582-583 over the union of the segments' rows. */
+int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
+                         int64_t nseg, double* out_gram, double* out_shift);
+/* pred[t][a] = beta[t-t0][0] + sum_j beta[t-t0][1+j] * x_cols[j][t][a] on grid rows with a mask
+ * bit (NaN elsewhere), t in [t0, t0+nt); beta_stride = 0 applies one coefficient vector. */
+int afm_predict_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda, int64_t t0,
+                    int64_t nt, const int32_t* cols, int p, const double* beta,
+                    int64_t beta_stride, const uint64_t* bits, double* pred);
+/* Fama-MacBeth over segments with rank > 0: mean_t beta_t and mean / (std / sqrt(T)). */
+int afm_fama_macbeth_f64(afm_ctx* ctx, const double* beta, const int32_t* rank, int64_t nseg,
+                         int k, double* mean_out, double* t_out);
+
 #ifdef __cplusplus
 }
 #endif
