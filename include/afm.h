@@ -86,6 +86,37 @@ int afm_predict_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_
 int afm_fama_macbeth_f64(afm_ctx* ctx, const double* beta, const int32_t* rank, int64_t nseg,
                          int k, double* mean_out, double* t_out);
 
+/* ---- K1-K3: rebalance, weights, PnL -- replaces PortfolioManager (KKT:795-892) ---------------
+ * Book arrays are [nd][2][AFM_MAX_BOOK] (long book, short book). */
+#define AFM_MAX_BOOK 64
+/* One call per set of rebalance dates (grid date indices `dates`, ascending, DEVICE int32[nd]).
+ * pred [T][lda] (NaN = no prediction); trad_bits: present in all_df AND in_trading_universe=='Y';
+ * hist/hist_bits: the history returns (df_train_y) and their presence; history rows are
+ * [h_t0, h_t1) when window <= 0 (the reference: the whole training window), else the `window`
+ * dates before each rebalance date; close/tmr: all_df close_price and tmr_ret1d.
+ * Outputs: k_out[nd] (book size), books (asset indices, long descending / short ascending by
+ * prediction, ties by ascending index), weights (exact min-variance, sum 1, lo <= w <= hi),
+ * sums[nd][4] = {sum(tmr*w) long, short (numpy pairwise), sum(w*close) long, short (sequential)},
+ * upos[nd][2][2][AFM_MAX_BOOK] / usize[nd][2]: members' positions in the id-union with the
+ * previous / next date's prediction set (turnover alignment), status[nd] (0 ok, 1 QP cap,
+ * 2 book larger than AFM_MAX_BOOK).  top_n <= AFM_MAX_BOOK. */
+int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, const int32_t* dates,
+                      int64_t nd, const double* pred, const uint64_t* trad_bits,
+                      const double* hist, const uint64_t* hist_bits, int64_t h_t0, int64_t h_t1,
+                      int64_t window, const double* close, const double* tmr, int top_n,
+                      double lo, double hi, int32_t* k_out, int32_t* books, double* weights,
+                      double* sums, int32_t* upos, int64_t* usize, int32_t* status);
+/* Value / turnover recursion over the nd rebalance dates (KKT:864-892): value[nd+1] (value[0] =
+ * v0), turnover[nd], long_ret[nd], short_ret[nd]. */
+int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out, const int32_t* books,
+                     const double* sums, const int32_t* upos, const int64_t* usize, double v0,
+                     double rate, double* value, double* turnover, double* long_ret,
+                     double* short_ret);
+/* determine_weights (KKT:817-833) for one book: R [rows][ld] returns (k columns, NaN = missing)
+ * -> pairwise-complete covariance cov[k][k] and the exact box-QP weights w[k]. */
+int afm_min_variance_weights_f64(afm_ctx* ctx, const double* R, int64_t rows, int64_t ld, int k,
+                                 double lo, double hi, double* w, double* cov, int32_t* status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -116,23 +116,24 @@ def select_books(ids: np.ndarray, vals: np.ndarray, tradable: np.ndarray, top_n:
     return long_ids, short_ids
 
 
-def book_history(hist_date, hist_id, hist_val, book, window: int | None = None, upto=None):
+def book_history(hist_date, hist_id, hist_val, book, window: int | None = None, upto=None,
+                 calendar=None):
     """KKT:858-859: history.swaplevel().loc[book].unstack().T -> [dates x book] with NaN holes.
-    ``window``/``upto`` restrict to the last ``window`` history dates before ``upto`` (north-star
-    rolling window); None reproduces the reference (the whole training window)."""
+    ``window``/``upto``/``calendar``: keep history dates in the ``window`` calendar dates that
+    precede ``upto`` (the north-star rolling window); None reproduces the reference (the whole
+    training window)."""
     m = np.isin(hist_id, book)
     missing = set(book.tolist()) - set(hist_id[m].tolist())
     if missing:
         raise KeyError(f"{sorted(missing)} not in history")
     d, i, v = hist_date[m], hist_id[m], hist_val[m]
-    if upto is not None:
-        k = d < upto
+    if window is not None:
+        cal = np.asarray(calendar)
+        j = int(np.searchsorted(cal, upto))
+        first = cal[max(0, j - window)]
+        k = (d >= first) & (d < upto)
         d, i, v = d[k], i[k], v[k]
     dates = np.unique(d)
-    if window is not None:
-        dates = dates[-window:]
-        k = np.isin(d, dates)
-        d, i, v = d[k], i[k], v[k]
     col = {x: j for j, x in enumerate(book.tolist())}
     R = np.full((len(dates), len(book)), np.nan)
     R[np.searchsorted(dates, d), [col[x] for x in i.tolist()]] = v
@@ -148,14 +149,17 @@ def run_portfolio(pred_date, pred_id, pred, hist_date, hist_id, hist, all_date, 
     cur = None                                   # (ids, positions) of the previous date
     akey = {(d, i): j for j, (d, i) in enumerate(zip(all_date.tolist(), all_id.tolist()))}
     udates = np.unique(pred_date)
+    calendar = np.unique(np.concatenate([pred_date, hist_date, all_date]))
     for dt in udates:
         m = pred_date == dt
         ids, vals = pred_id[m], pred[m]
         rows = np.array([akey.get((dt, i), -1) for i in ids.tolist()])
         trad = np.array([r >= 0 and bool(all_tradable[r]) for r in rows])
         L, S = select_books(ids, vals, trad, top_n)
-        wl = box_qp_weights(pairwise_cov(book_history(hist_date, hist_id, hist, L, window, dt if window else None)), lo, hi)[0]
-        ws = box_qp_weights(pairwise_cov(book_history(hist_date, hist_id, hist, S, window, dt if window else None)), lo, hi)[0]
+        wl = box_qp_weights(pairwise_cov(book_history(hist_date, hist_id, hist, L, window, dt,
+                                                      calendar)), lo, hi)[0]
+        ws = box_qp_weights(pairwise_cov(book_history(hist_date, hist_id, hist, S, window, dt,
+                                                      calendar)), lo, hi)[0]
         books += [L, S]
         weights += [wl, ws]
         size = V[-1] / 2

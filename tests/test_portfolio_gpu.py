@@ -1,0 +1,100 @@
+"""GPU parity of the rebalance / weights / PnL path (K1-K4) against the reference's own outputs
+(bit-exact where the reference is deterministic) and the exact-QP oracle (rel 1e-9)."""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from helpers import same
+
+pytestmark = pytest.mark.gpu
+
+
+def frames(g):
+    pred = pd.DataFrame({"lr_predict": g["pred"]}, index=pd.MultiIndex.from_arrays(
+        [g["pred_date"].astype("datetime64[ns]"), g["pred_id"]]))
+    hist = pd.DataFrame({"target": g["hist"]}, index=pd.MultiIndex.from_arrays(
+        [g["hist_date"].astype("datetime64[ns]"), g["hist_id"]]))
+    all_df = pd.DataFrame({"in_trading_universe": np.where(g["all_tradable"], "Y", "N"),
+                           "close_price": g["all_close"], "tmr_ret1d": g["all_tmr"]},
+                          index=pd.MultiIndex.from_arrays(
+                              [g["all_date"].astype("datetime64[ns]"), g["all_id"]],
+                              names=["data_date", "security_id"]))
+    return pred, hist, all_df
+
+
+def test_portfolio_manager_matches_reference(golden_dir):
+    from afm.portfolio import PortfolioManager
+    g = np.load(os.path.join(golden_dir, "portfolio_pipeline.npz"))
+    pred, hist, all_df = frames(g)
+    pm = PortfolioManager(pred, hist, all_df)
+    pm.calculate_portfolio()
+    assert same(np.asarray(pm.portfolio_value["Portfolio"], dtype=np.float64), g["value"])
+    assert same(np.asarray(pm.turnovers, dtype=np.float64), g["turnover"])
+    assert same(np.asarray(pm.long_returns), g["long_ret"])
+    assert same(np.asarray(pm.short_returns), g["short_ret"])
+    ids = np.concatenate([np.r_[L, S] for _, L, S in pm.books]).astype(np.int64)
+    assert same(ids, g["book_ids"])
+    assert pm.calculate_sharpe_ratio() == g["sharpe"]
+    assert pm.annualized_return() == g["ann_ret"]
+    assert pm.max_drawdown() == g["mdd"]
+
+
+@pytest.mark.parametrize("n", [10, 9, 20, 30])
+def test_determine_weights(golden_dir, n):
+    from afm.portfolio import min_variance_weights
+    from oracle import portfolio as P
+    g = np.load(os.path.join(golden_dir, "weights_cases.npz"))
+    R = g[f"n{n}_ret"]
+    w, cov = min_variance_weights(R)
+    ref_cov = g[f"n{n}_cov"]
+    if np.isnan(R).any():
+        assert same(cov, ref_cov)                    # nancorr(cov=True): bit-exact Welford
+    else:
+        assert np.abs(cov - ref_cov).max() <= 1e-13 * np.abs(ref_cov).max()
+    wo, _ = P.box_qp_weights(P.pairwise_cov(R))
+    if n in (9, 10):
+        assert same(w, np.full(n, 0.1))
+    else:
+        assert np.abs(w - wo).max() < 1e-9
+        assert abs(w.sum() - 1) < 1e-13
+
+
+@pytest.mark.parametrize("top_n,window", [(10, 60), (20, 120), (3, None)])
+def test_rolling_window_books_vs_oracle(top_n, window):
+    """North-star rolling history window and bounded (top_n > 10) books vs the oracle."""
+    from afm.portfolio import PortfolioManager
+    from oracle import portfolio as P
+    rng = np.random.default_rng(top_n)
+    T, A = 160, 48
+    dates = np.asarray(np.busday_offset(np.datetime64("2016-01-04"), np.arange(T), roll="forward"),
+                       dtype="datetime64[ns]")
+    ids = 2000 + 3 * np.arange(A)
+    present = rng.random((T, A)) < 0.93
+    tt, aa = np.nonzero(present)
+    d, i = dates[tt], ids[aa]
+    ret = rng.normal(0, 0.02, len(tt))
+    close = 50 * np.exp(rng.normal(0, 0.1, len(tt)))
+    trad = rng.random(len(tt)) < 0.9
+    hist_m = tt < 100
+    test_m = tt >= 100
+    pred_v = rng.normal(size=test_m.sum())
+    pred = pd.DataFrame({"p": pred_v}, index=pd.MultiIndex.from_arrays([d[test_m], i[test_m]]))
+    hist = pd.DataFrame({"target": ret[hist_m]}, index=pd.MultiIndex.from_arrays([d[hist_m], i[hist_m]]))
+    all_df = pd.DataFrame({"in_trading_universe": np.where(trad, "Y", "N"), "close_price": close,
+                           "tmr_ret1d": ret}, index=pd.MultiIndex.from_arrays([d, i]))
+    pm = PortfolioManager(pred, hist, all_df, top_n=top_n, window=window)
+    pm.calculate_portfolio()
+    o = P.run_portfolio(d[test_m].astype(np.int64), i[test_m], pred_v,
+                        d[hist_m].astype(np.int64), i[hist_m], ret[hist_m],
+                        d.astype(np.int64), i, trad, close, ret, top_n=top_n,
+                        window=window if window else None)
+    # the oracle's rolling window counts history DATES; the GPU counts grid dates (the same here:
+    # every calendar date carries history rows)
+    for (dt, L, S), Lo, So in zip(pm.books, o["books"][0::2], o["books"][1::2]):
+        assert L == Lo.tolist() and S == So.tolist()
+    v = np.asarray(pm.portfolio_value["Portfolio"], dtype=np.float64)
+    assert np.abs(v - o["value"]).max() / o["value"].max() < 1e-12
+    assert np.abs(np.asarray(pm.turnovers, dtype=np.float64) - o["turnover"]).max() <= \
+        1e-9 * max(1.0, o["turnover"].max())
