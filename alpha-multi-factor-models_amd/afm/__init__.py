@@ -15,6 +15,9 @@ from .factors import FACTOR_NAMES, compute_factors, factor_panel  # noqa: F401
 from .grid import PanelGrid, pack_bits, unpack_bits  # noqa: F401
 from . import regression  # noqa: F401
 from .regression import LinearRegression, cross_sectional_ols  # noqa: F401
+from .analyzer import AlphaSignalAnalyzer  # noqa: F401
+from .portfolio import PortfolioManager  # noqa: F401
 
 __all__ = ["compute_factors", "factor_panel", "FACTOR_NAMES", "PanelGrid", "pack_bits",
-           "unpack_bits"]
+           "unpack_bits", "LinearRegression", "cross_sectional_ols", "AlphaSignalAnalyzer",
+           "PortfolioManager"]

@@ -1,0 +1,556 @@
+// Signal evaluation: AlphaSignalAnalyzer.run() without plotting
+// ("KKT Yuliang Jiang.py":298-375), on calendar grids, bit-exact with pandas 2.3.3.
+//
+//  fwd_returns_kernel   A1  k-th next present price row per asset (k = 1, 2, 5): c'/c - 1, kept
+//                           when <= 1 (KKT:311-312); one thread per cell, presence-word scans.
+//  xs_prepare_kernel    A1  per date (one workgroup): the merge/dropna cascade of KKT:313 and the
+//                           per-date demean of KKT:315-318 -- mean = numpy pairwise sum / n over
+//                           the rows surviving each step, evaluated with numpy's exact tree
+//                           (leaves in parallel, combine in order); writes the surviving rows
+//                           compacted (ascending security id = the reference's row order).
+//  xs_rank_kernel       A3/A4 per date: exact ranks (method='first': ties by row position),
+//                           ascending and descending, from 2048-row LDS bitonic-sorted chunks +
+//                           binary-search merge counts.
+//  xs_stats_kernel      A2-A4 one lane per (date, return type): pandas nancorr Welford IC
+//                           (return = the later column), Kahan group means per decile layer
+//                           (layer = int(rank/n*10)+1, KKT:328-330), factor-weighted top-10
+//                           returns summed in the string-sorted pivot column order (KKT:362-369).
+//  xs_series_kernel     A2-A4 cumulative layer / long-short / top-k series and the per-year IR
+//                           (pairwise mean / two-pass std of the IC values, KKT:353).
+#include "afm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace afm {
+namespace {
+
+typedef unsigned long long u64;
+constexpr int kT = 256;
+constexpr int kChunk = 2048;          // rows per LDS-sorted chunk
+constexpr int kMaxLeaves = 1024;      // pairwise leaves (n <= 65536)
+constexpr int kTopK = 10;
+constexpr int kLayers = 10;
+
+__device__ __forceinline__ double qnan() { return __builtin_nan(""); }
+__device__ __forceinline__ bool bit_at(const uint64_t* bits, int64_t lda, int64_t t, int64_t a) {
+    return (bits[(t >> 6) * lda + a] >> (t & 63)) & 1ull;
+}
+__device__ __forceinline__ u64 okey(double v) {
+    if (v == 0.0) v = 0.0;
+    u64 u = (u64)__double_as_longlong(v);
+    return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+
+// ---- A1: forward returns -------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fwd_returns_kernel(int64_t T, int64_t lda,
+                                                          const double* close,
+                                                          const uint64_t* pbits, double* fr) {
+    const int64_t a = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int64_t t = (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (t >= T) return;
+    const int64_t plane = T * lda;
+    const int64_t cell = t * lda + a;
+    double r[3] = {qnan(), qnan(), qnan()};
+    if (bit_at(pbits, lda, t, a)) {
+        const int ks[3] = {1, 2, 5};
+        const int64_t nch = (T + 63) / 64;
+        int64_t ch = t >> 6;
+        const int s = (int)(t & 63);
+        u64 w = pbits[ch * lda + a];
+        u64 rest = (s == 63) ? 0ull : (w >> (s + 1)) << (s + 1);
+        int found = 0;
+        int64_t nxt[5];
+        while (found < 5) {
+            while (rest && found < 5) {
+                nxt[found++] = ch * 64 + __builtin_ctzll(rest);
+                rest &= rest - 1;
+            }
+            if (found >= 5 || ++ch >= nch) break;
+            rest = pbits[ch * lda + a];
+        }
+        const double c0 = close[cell];
+        for (int q = 0; q < 3; ++q) {
+            if (found >= ks[q]) {
+                double v = close[nxt[ks[q] - 1] * lda + a] / c0 - 1;
+                r[q] = (v <= 1) ? v : qnan();       // return_data[return_data[i] <= 1]
+            }
+        }
+    }
+    for (int q = 0; q < 3; ++q) fr[q * plane + cell] = r[q];
+}
+
+// ---- block helpers ---------------------------------------------------------------------------
+__device__ int block_scan(int v, int* sbuf, int* excl) {
+    const int tid = threadIdx.x;
+    sbuf[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < kT; off <<= 1) {
+        int x = tid >= off ? sbuf[tid - off] : 0;
+        __syncthreads();
+        sbuf[tid] += x;
+        __syncthreads();
+    }
+    *excl = sbuf[tid] - v;
+    int total = sbuf[kT - 1];
+    __syncthreads();
+    return total;
+}
+
+struct PwShared {
+    int64_t loff[kMaxLeaves];
+    int llen[kMaxLeaves];
+    double lval[kMaxLeaves];
+    int nleaves;
+    int cursor;
+    double result;
+};
+
+__device__ void pw_enum(PwShared& p, int64_t off, int64_t n) {
+    if (n <= 128) {
+        p.loff[p.nleaves] = off;
+        p.llen[p.nleaves] = (int)n;
+        p.nleaves++;
+        return;
+    }
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    pw_enum(p, off, n2);
+    pw_enum(p, off + n2, n - n2);
+}
+
+__device__ double pw_combine(PwShared& p, int64_t n) {
+    if (n <= 128) return p.lval[p.cursor++];
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    double a = pw_combine(p, n2);
+    double b = pw_combine(p, n - n2);
+    return a + b;
+}
+
+__device__ double leaf_sum(const double* a, int n) {
+    if (n < 8) {
+        double res = 0.;
+        for (int i = 0; i < n; ++i) res += a[i];
+        return res;
+    }
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i;
+    for (i = 8; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+}
+
+// np.add.reduce of v[0..n) (0.0 + numpy pairwise sum), evaluated by the whole block
+__device__ double block_np_sum(PwShared& p, const double* v, int64_t n) {
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        p.nleaves = 0;
+        p.cursor = 0;
+        if (n > 0) pw_enum(p, 0, n);
+    }
+    __syncthreads();
+    for (int l = tid; l < p.nleaves; l += kT) p.lval[l] = leaf_sum(v + p.loff[l], p.llen[l]);
+    __syncthreads();
+    if (tid == 0) p.result = n > 0 ? 0.0 + pw_combine(p, n) : 0.0;
+    __syncthreads();
+    double r = p.result;
+    __syncthreads();
+    return r;
+}
+
+// ---- A1: per-date merge/dropna cascade + demean --------------------------------------------
+struct PrepArgs {
+    int64_t T, lda, A;
+    const double* sig;        // [T][lda] signal (NaN = no row)
+    const double* fr;         // [3][T][lda] forward returns
+    double* scratch;          // [T][lda] compaction scratch
+    double* rows;             // [4][T][lda]: factor, r1, r2, r5 of surviving rows, compacted
+    int32_t* rows_idx;        // [T][lda] asset index of each compacted row
+    int32_t* nrows;           // [T] surviving rows per date
+};
+
+__global__ __launch_bounds__(kT) void xs_prepare_kernel(PrepArgs g) {
+    __shared__ PwShared pw;
+    __shared__ int sbuf[kT];
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x;
+    const int64_t plane = g.T * g.lda;
+    const double* sig = g.sig + t * g.lda;
+    double* scr = g.scratch + t * g.lda;
+    double mu[3];
+    for (int k = 0; k < 3; ++k) {
+        // rows surviving step k: signal and returns 1..k all present
+        int n = 0;
+        for (int64_t base = 0; base < g.A; base += kT) {
+            const int64_t a = base + tid;
+            int ok = 0;
+            double v = 0.0;
+            if (a < g.A) {
+                ok = sig[a] == sig[a];
+                for (int q = 0; q <= k && ok; ++q) {
+                    double r = g.fr[q * plane + t * g.lda + a];
+                    ok = r == r;
+                }
+                v = g.fr[k * plane + t * g.lda + a];
+            }
+            int ex;
+            const int tot = block_scan(ok, sbuf, &ex);
+            if (ok) scr[n + ex] = v;
+            n += tot;
+        }
+        __syncthreads();
+        mu[k] = n > 0 ? block_np_sum(pw, scr, n) / (double)n : qnan();
+    }
+    // final rows (all three returns), compacted with demeaned returns
+    int n = 0;
+    for (int64_t base = 0; base < g.A; base += kT) {
+        const int64_t a = base + tid;
+        int ok = 0;
+        if (a < g.A) {
+            ok = sig[a] == sig[a];
+            for (int q = 0; q < 3 && ok; ++q) {
+                double r = g.fr[q * plane + t * g.lda + a];
+                ok = r == r;
+            }
+        }
+        int ex;
+        const int tot = block_scan(ok, sbuf, &ex);
+        if (ok) {
+            const int64_t o = t * g.lda + n + ex;
+            g.rows[o] = sig[a];
+            for (int q = 0; q < 3; ++q) g.rows[(1 + q) * plane + o] = g.fr[q * plane + t * g.lda + a] - mu[q];
+            g.rows_idx[o] = (int32_t)a;
+        }
+        n += tot;
+    }
+    if (tid == 0) g.nrows[t] = n;
+}
+
+// ---- A3/A4: exact ranks -------------------------------------------------------------------
+struct RankArgs {
+    int64_t T, lda;
+    const double* rows;       // factor column of the compacted rows
+    const int32_t* nrows;
+    u64* skey;                // [T][lda] sorted chunk keys
+    int32_t* sidx;            // [T][lda] sorted chunk positions
+    int32_t* rank_asc;        // [T][lda]
+    int32_t* rank_desc;       // [T][lda]
+};
+
+__global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g) {
+    __shared__ u64 key[kChunk];
+    __shared__ int32_t idx[kChunk];
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x;
+    const int n = g.nrows[t];
+    const int64_t base = t * g.lda;
+    const int nch = (n + kChunk - 1) / kChunk;
+    for (int c = 0; c < nch; ++c) {
+        const int c0 = c * kChunk, len = min(kChunk, n - c0);
+        for (int e = tid; e < kChunk; e += kT) {
+            if (e < len) {
+                key[e] = okey(g.rows[base + c0 + e]);
+                idx[e] = c0 + e;
+            } else {
+                key[e] = ~0ull;
+                idx[e] = 0x7fffffff;
+            }
+        }
+        __syncthreads();
+        // bitonic sort of (key, idx) ascending
+        for (int size = 2; size <= kChunk; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int e = tid; e < kChunk / 2; e += kT) {
+                    const int lo = 2 * e - (e & (stride - 1));
+                    const int hi = lo + stride;
+                    const bool up = ((lo & size) == 0);
+                    const u64 ka = key[lo], kb = key[hi];
+                    const int ia = idx[lo], ib = idx[hi];
+                    const bool gt = (ka > kb) || (ka == kb && ia > ib);
+                    if (gt == up) {
+                        key[lo] = kb; key[hi] = ka;
+                        idx[lo] = ib; idx[hi] = ia;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int e = tid; e < len; e += kT) {
+            g.skey[base + c0 + e] = key[e];
+            g.sidx[base + c0 + e] = idx[e];
+        }
+        __syncthreads();
+    }
+    // rank of every row = sum over chunks of its lower-bound position (keys then row position)
+    for (int e = tid; e < n; e += kT) {
+        const u64 k0 = okey(g.rows[base + e]);
+        int less = 0, greater = 0;
+        for (int c = 0; c < nch; ++c) {
+            const int c0 = c * kChunk, len = min(kChunk, n - c0);
+            const u64* K = g.skey + base + c0;
+            const int32_t* I = g.sidx + base + c0;
+            // lb: first position with (key, idx) >= (k0, e)
+            int lo = 0, hi = len;
+            while (lo < hi) {
+                int m = (lo + hi) >> 1;
+                if (K[m] < k0 || (K[m] == k0 && I[m] < e)) lo = m + 1; else hi = m;
+            }
+            const int lb = lo;
+            // first key >= k0, first key > k0
+            lo = 0; hi = len;
+            while (lo < hi) { int m = (lo + hi) >> 1; if (K[m] < k0) lo = m + 1; else hi = m; }
+            const int lbk = lo;
+            lo = 0; hi = len;
+            while (lo < hi) { int m = (lo + hi) >> 1; if (K[m] <= k0) lo = m + 1; else hi = m; }
+            const int ubk = lo;
+            less += lb;                              // key < k0, or equal and earlier
+            greater += (len - ubk) + (lb - lbk);     // key > k0, or equal and earlier
+        }
+        g.rank_asc[base + e] = less + 1;
+        g.rank_desc[base + e] = greater + 1;
+    }
+}
+
+// ---- A2-A4: per (date, return type) sequential statistics --------------------------------------
+struct StatArgs {
+    int64_t T, lda;
+    const int32_t* dates;     // [nd] dates to evaluate
+    int64_t nd;
+    const double* rows;       // [4][T][lda]
+    const int32_t* nrows;
+    const int32_t* rank_asc;
+    const int32_t* rank_desc;
+    int mcols;                // pivot columns present (ranks 1..mcols)
+    double* ic;               // [nd][3]
+    double* layer_mean;       // [nd][3][10]
+    int32_t* layer_cnt;       // [nd][10]
+    double* port;             // [nd][3]
+};
+
+__global__ __launch_bounds__(64) void xs_stats_kernel(StatArgs g) {
+    const int64_t gid = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (gid >= g.nd * 3) return;
+    const int64_t di = gid / 3;
+    const int k = (int)(gid % 3);
+    const int64_t t = g.dates[di];
+    const int n = g.nrows[t];
+    const int64_t plane = g.T * g.lda;
+    const int64_t base = t * g.lda;
+    const double* F = g.rows + base;
+    const double* Rk = g.rows + (1 + k) * plane + base;
+    // nancorr(return_k, factor): vx = return (later column), vy = factor
+    double nobs = 0, mx = 0, my = 0, sxx = 0, syy = 0, sxy = 0;
+    double lsum[kLayers], lcomp[kLayers];
+    int lcnt[kLayers];
+    for (int l = 0; l < kLayers; ++l) { lsum[l] = 0; lcomp[l] = 0; lcnt[l] = 0; }
+    double pv_f[kTopK], pv_r[kTopK];
+    bool pv_has[kTopK];
+    for (int j = 0; j < kTopK; ++j) { pv_f[j] = qnan(); pv_r[j] = qnan(); pv_has[j] = false; }
+    for (int e = 0; e < n; ++e) {
+        const double vy = F[e], vx = Rk[e];
+        if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
+            nobs += 1;
+            const double dx = vx - mx, dy = vy - my;
+            mx += 1. / nobs * dx;
+            my += 1. / nobs * dy;
+            sxx += (vx - mx) * dx;
+            syy += (vy - my) * dy;
+            sxy += (vx - mx) * dy;
+        }
+        // layer (KKT:328-330) and Kahan group mean (groupby(['date','layer']).mean())
+        const double pct = (double)g.rank_asc[base + e] / (double)n;
+        int layer = (int)(pct * kLayers) + 1;
+        if (layer > kLayers) layer = kLayers;
+        const int l = layer - 1;
+        if (vx == vx) {
+            lcnt[l] += 1;
+            const double y = vx - lcomp[l];
+            const double tt = lsum[l] + y;
+            lcomp[l] = tt - lsum[l] - y;
+            if (lcomp[l] != lcomp[l]) lcomp[l] = 0;
+            lsum[l] = tt;
+        }
+        const int rd = g.rank_desc[base + e];
+        if (rd <= kTopK) {
+            pv_f[rd - 1] = vy;
+            pv_r[rd - 1] = vx;
+            pv_has[rd - 1] = true;
+        }
+    }
+    double r = qnan();
+    if (nobs >= 1) {
+        const double div = __builtin_sqrt(sxx * syy);
+        if (div != 0) r = sxy / div;
+    }
+    g.ic[di * 3 + k] = r;
+    for (int l = 0; l < kLayers; ++l) {
+        g.layer_mean[(di * 3 + k) * kLayers + l] = lcnt[l] ? lsum[l] / (double)lcnt[l] : qnan();
+        if (k == 0) g.layer_cnt[di * kLayers + l] = lcnt[l];
+    }
+    // pivot columns in string order '1.0','10.0','2.0',...,'9.0' (or 1..m for m < 10)
+    int order[kTopK];
+    int m = g.mcols;
+    if (m >= 10) {
+        order[0] = 1; order[1] = 10;
+        for (int j = 2; j < 10; ++j) order[j] = j;
+    } else {
+        for (int j = 0; j < m; ++j) order[j] = j + 1;
+    }
+    double row[kTopK];
+    for (int j = 0; j < m; ++j) {
+        const double f = pv_has[order[j] - 1] ? pv_f[order[j] - 1] : qnan();
+        row[j] = f == f ? f : 0.0;
+    }
+    const double wsum = leaf_sum(row, m);
+    for (int j = 0; j < m; ++j) {
+        const int q = order[j] - 1;
+        double v = qnan();
+        if (pv_has[q]) v = pv_r[q] * (pv_f[q] / wsum);
+        row[j] = v == v ? v : 0.0;
+    }
+    g.port[di * 3 + k] = leaf_sum(row, m);
+}
+
+// ---- series: cumulative layers / long-short / top-k, per-year IR -----------------------------
+__device__ double seq_pairwise(const double* a, int64_t n) {   // np.add.reduce, single thread
+    if (n <= 128) return leaf_sum(a, (int)n);
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return seq_pairwise(a, n2) + seq_pairwise(a + n2, n - n2);
+}
+
+__global__ void xs_series_kernel(int64_t nd, const double* layer_mean, const double* port,
+                                 const double* ic, const int32_t* year, int nyears, int year0,
+                                 double* cum_layer, double* ls, double* cum_port, double* ir,
+                                 double* scratch) {
+    const int tid = threadIdx.x;
+    if (tid < 30) {                                        // (type, layer) cumsum, NaN-skipping
+        const int k = tid / 10, l = tid % 10;
+        double s = 0.0;
+        for (int64_t i = 0; i < nd; ++i) {
+            const double x = layer_mean[(i * 3 + k) * kLayers + l];
+            if (x == x) {
+                s = s + x;
+                cum_layer[(i * 3 + k) * kLayers + l] = s;
+            } else {
+                cum_layer[(i * 3 + k) * kLayers + l] = qnan();
+            }
+        }
+    } else if (tid < 33) {
+        const int k = tid - 30;
+        double s = 0.0;
+        for (int64_t i = 0; i < nd; ++i) {
+            s = s + port[i * 3 + k];
+            cum_port[i * 3 + k] = s;
+        }
+    }
+    __syncthreads();
+    if (tid < 15) {                                        // long-short: cum[10-l+1] - cum[l]
+        const int k = tid / 5, l = tid % 5 + 1;
+        for (int64_t i = 0; i < nd; ++i)
+            ls[(i * 3 + k) * 5 + (l - 1)] =
+                cum_layer[(i * 3 + k) * kLayers + (kLayers - l)] - cum_layer[(i * 3 + k) * kLayers + (l - 1)];
+    }
+    if (tid >= 64 && tid < 64 + 3 * nyears) {              // IR per (year, type)
+        const int q = tid - 64;
+        const int y = q / 3, k = q % 3;
+        double* buf = scratch + (int64_t)q * nd;
+        int64_t n = 0;
+        for (int64_t i = 0; i < nd; ++i) {
+            const double x = ic[i * 3 + k];
+            if (year[i] == year0 + y && x == x) buf[n++] = x;
+        }
+        double res = qnan();
+        if (n > 0) {
+            const double mean = (0.0 + seq_pairwise(buf, n)) / (double)n;
+            double sd = qnan();
+            if (n > 1) {
+                const double avg = (0.0 + seq_pairwise(buf, n)) / (double)n;
+                for (int64_t i = 0; i < n; ++i) {
+                    const double d = avg - buf[i];
+                    buf[i] = d * d;
+                }
+                sd = __builtin_sqrt((0.0 + seq_pairwise(buf, n)) / ((double)n - 1.0));
+            }
+            res = mean / sd;
+        }
+        ir[y * 3 + k] = res;
+    }
+}
+
+}  // namespace
+}  // namespace afm
+
+using namespace afm;
+
+extern "C" int afm_fwd_returns_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* close,
+                                   const uint64_t* price_bits, double* fr) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && lda > 0 && lda % 64 == 0, "bad shape");
+    AFM_CHECK_ARG(close && price_bits && fr, "null buffer");
+    dim3 grid((unsigned)(lda / 64), (unsigned)((T + 3) / 4));
+    hipLaunchKernelGGL(fwd_returns_kernel, grid, dim3(256), 0, ctx->stream, T, lda, close,
+                       price_bits, fr);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_xs_prepare_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
+                                  const double* sig, const double* fr, double* scratch,
+                                  double* rows, int32_t* rows_idx, int32_t* nrows) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && A > 0 && lda >= A && lda % 64 == 0 && A <= 65536, "bad shape");
+    AFM_CHECK_ARG(sig && fr && scratch && rows && rows_idx && nrows, "null buffer");
+    PrepArgs g{T, lda, A, sig, fr, scratch, rows, rows_idx, nrows};
+    hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)T), dim3(kT), 0, ctx->stream, g);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* rows,
+                               const int32_t* nrows, uint64_t* skey, int32_t* sidx,
+                               int32_t* rank_asc, int32_t* rank_desc) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && lda % 64 == 0, "bad shape");
+    AFM_CHECK_ARG(rows && nrows && skey && sidx && rank_asc && rank_desc, "null buffer");
+    RankArgs g{T, lda, rows, nrows, (u64*)skey, sidx, rank_asc, rank_desc};
+    hipLaunchKernelGGL(xs_rank_kernel, dim3((unsigned)T), dim3(kT), 0, ctx->stream, g);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_xs_stats_f64(afm_ctx* ctx, int64_t T, int64_t lda, const int32_t* dates,
+                                int64_t nd, const double* rows, const int32_t* nrows,
+                                const int32_t* rank_asc, const int32_t* rank_desc, int mcols,
+                                double* ic, double* layer_mean, int32_t* layer_cnt,
+                                double* port) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(mcols >= 0 && mcols <= kTopK, "mcols must be in [0, 10]");
+    AFM_CHECK_ARG(dates && rows && nrows && rank_asc && rank_desc && ic && layer_mean &&
+                      layer_cnt && port, "null buffer");
+    if (nd <= 0) return AFM_OK;
+    StatArgs g{T, lda, dates, nd, rows, nrows, rank_asc, rank_desc, mcols, ic, layer_mean,
+               layer_cnt, port};
+    hipLaunchKernelGGL(xs_stats_kernel, dim3((unsigned)((nd * 3 + 63) / 64)), dim3(64), 0,
+                       ctx->stream, g);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_xs_series_f64(afm_ctx* ctx, int64_t nd, const double* layer_mean,
+                                 const double* port, const double* ic, const int32_t* year,
+                                 int nyears, int year0, double* cum_layer, double* ls,
+                                 double* cum_port, double* ir, double* scratch) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(nyears >= 0 && 64 + 3 * nyears <= 1024, "too many years (max 320)");
+    AFM_CHECK_ARG(layer_mean && port && ic && year && cum_layer && ls && cum_port && ir &&
+                      scratch, "null buffer");
+    if (nd <= 0) return AFM_OK;
+    hipLaunchKernelGGL(xs_series_kernel, dim3(1), dim3(1024), 0, ctx->stream, nd, layer_mean,
+                       port, ic, year, nyears, year0, cum_layer, ls, cum_port, ir, scratch);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}

@@ -117,6 +117,38 @@ int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out, const int32
 int afm_min_variance_weights_f64(afm_ctx* ctx, const double* R, int64_t rows, int64_t ld, int k,
                                  double lo, double hi, double* w, double* cov, int32_t* status);
 
+/* ---- A1-A4: signal evaluation -- replaces AlphaSignalAnalyzer.run (KKT:298-375) ----------
+ * fr [3][T][lda]: k-th next present price row return c'/c - 1 for k = 1, 2, 5, NaN unless <= 1
+ * (KKT:311-312); price_bits: presence of price_data rows. */
+int afm_fwd_returns_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* close,
+                        const uint64_t* price_bits, double* fr);
+/* Per date: the merge/dropna cascade and per-date demeans of KKT:313-318 (numpy pairwise mean).
+ * sig [T][lda] (NaN = no signal row).  Surviving rows, compacted in ascending asset order:
+ * rows [4][T][lda] = {factor, return_1, return_2, return_5 (demeaned)}, rows_idx [T][lda] asset
+ * index, nrows [T].  scratch [T][lda].  A <= 65536. */
+int afm_xs_prepare_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, const double* sig,
+                       const double* fr, double* scratch, double* rows, int32_t* rows_idx,
+                       int32_t* nrows);
+/* Exact per-date ranks of the compacted factor column (method='first': ties by row order),
+ * ascending and descending.  skey/sidx [T][lda] scratch. */
+int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* rows,
+                    const int32_t* nrows, uint64_t* skey, int32_t* sidx, int32_t* rank_asc,
+                    int32_t* rank_desc);
+/* For the nd dates (DEVICE int32 grid indices): IC [nd][3] (nancorr Welford, KKT:344-345),
+ * decile layer means [nd][3][10] and counts [nd][10] (KKT:328-332), top-10 factor-weighted
+ * returns port [nd][3] (KKT:359-369; mcols = pivot columns present, <= 10). */
+int afm_xs_stats_f64(afm_ctx* ctx, int64_t T, int64_t lda, const int32_t* dates, int64_t nd,
+                     const double* rows, const int32_t* nrows, const int32_t* rank_asc,
+                     const int32_t* rank_desc, int mcols, double* ic, double* layer_mean,
+                     int32_t* layer_cnt, double* port);
+/* Cumulative layers [nd][3][10], long-short [nd][3][5] (cum[10-l+1] - cum[l]), cumulative
+ * top-10 returns [nd][3], IR [nyears][3] (year[nd] DEVICE int32, years year0..year0+nyears-1);
+ * scratch [3*nyears][nd]. */
+int afm_xs_series_f64(afm_ctx* ctx, int64_t nd, const double* layer_mean, const double* port,
+                      const double* ic, const int32_t* year, int nyears, int year0,
+                      double* cum_layer, double* ls, double* cum_port, double* ir,
+                      double* scratch);
+
 #ifdef __cplusplus
 }
 #endif
