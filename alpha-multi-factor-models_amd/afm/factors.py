@@ -32,12 +32,13 @@ COL = {n: i for i, n in enumerate(FACTOR_NAMES)}
 TARGET, TMR = COL["target"], COL["tmr_ret1d"]
 
 
-def factor_panel(grid: PanelGrid, out=None, nanfree=None):
+def factor_panel(grid: PanelGrid, out=None, nanfree=None, finite=None):
     """Run the factor kernel on a device-resident grid.
 
     Returns ``(out, nanfree)``: ``out`` torch float64 ``[98][T][lda]`` (absent cells untouched,
     NaN-initialised when allocated here), ``nanfree`` int64 ``[ceil(T/64)][lda]`` presence-and-
-    no-NaN-in-96-factors bits (afm.h)."""
+    no-NaN-in-96-factors bits (afm.h).  ``finite`` (optional, preallocated like ``nanfree``)
+    receives the presence-and-all-96-finite bits."""
     import torch
     ctx = _lib.Context.get(grid.device.index)
     T, lda = grid.T, grid.lda
@@ -51,7 +52,8 @@ def factor_panel(grid: PanelGrid, out=None, nanfree=None):
     P = _lib.ptr
     _lib.check(_lib.lib().afm_factors_f64(
         ctx.bind_stream(), T, grid.A, lda, P(grid.close), P(grid.volume), P(grid.ret1d),
-        P(grid.excess), P(grid.vbits), P(out), P(nanfree)), "afm_factors_f64")
+        P(grid.excess), P(grid.vbits), P(out), P(nanfree),
+        P(finite) if finite is not None else None), "afm_factors_f64")
     return out, nanfree
 
 

@@ -58,6 +58,7 @@ class PanelGrid:
     valid: object              # torch [T][lda] bool
     vbits: object              # torch [ceil(T/64)][lda] int64 (uint64 bit pattern)
     tradable: object = None    # torch [T][lda] bool
+    tbits: object = None       # torch [ceil(T/64)][lda] present AND tradable bits
 
     @property
     def T(self) -> int:
@@ -87,9 +88,10 @@ class PanelGrid:
             return torch.from_numpy(np.ascontiguousarray(x)).to(device=dev, dtype=dt)
 
         valid = up(p.valid, torch.bool)
+        trad = up(p.tradable, torch.bool)
         return cls(dates=p.dates, ids=p.ids, close=up(p.close), volume=up(p.volume),
                    ret1d=up(p.ret1d), excess=up(p.excess), valid=valid, vbits=pack_bits(valid),
-                   tradable=up(p.tradable, torch.bool))
+                   tradable=trad, tbits=pack_bits(trad & valid))
 
     @classmethod
     def from_frame(cls, df, device=None):
@@ -124,5 +126,6 @@ class PanelGrid:
             trad[ti, ai] = torch.from_numpy(df["in_trading_universe"].to_numpy() == "Y").to(dev)
         g = cls(dates=np.asarray(dates, dtype="datetime64[ns]"), ids=ids.astype(np.int64),
                 close=plane("close_price"), volume=plane("volume"), ret1d=plane("ret1d"),
-                excess=plane("excess_ret1d"), valid=valid, vbits=pack_bits(valid), tradable=trad)
+                excess=plane("excess_ret1d"), valid=valid, vbits=pack_bits(valid), tradable=trad,
+                tbits=pack_bits(trad & valid) if trad is not None else None)
         return g, ti, ai

@@ -1,0 +1,159 @@
+"""The end-to-end hot path on one device: factor build -> cross-sectional regression -> KKT
+weights -> PnL (BASELINE.json ``metric``).
+
+One ``step()`` over a device-resident calendar-grid panel:
+
+1. factors       afm_factors_f64: 98 planes + dropna / finite row masks
+2. xs gram       afm_xs_gram_f64: per-date Gram of [1, 96 factors, target] on fp64 MFMA
+3. xs solve      afm_ols_solve_f64 + afm_fama_macbeth_f64: per-date betas, FM mean / t
+4. pooled OLS    afm_pool_moments_f64 + solve over the train+valid dates (the reference's
+                 LinearRegression, KKT:582-583)
+5. predict       afm_predict_f64 on the test dates
+6. rebalance     afm_rebalance_f64: per test date top/bottom-n selection, rolling-window
+                 pairwise covariance, exact box-QP weights (KKT:842-892)
+7. pnl           afm_pnl_scan_f64: value / turnover recursion
+
+All buffers are allocated once; every stage runs on torch's current stream, so a step is a
+straight sequence of kernel launches (no host synchronisation inside).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .factors import N_FACTORS, TARGET
+from .grid import PanelGrid
+from .portfolio import MAX_BOOK
+
+STAGES = ("factors", "xs_gram", "xs_solve", "pooled_ols", "predict", "rebalance", "pnl")
+
+
+@dataclass
+class PipelineConfig:
+    cols: list = field(default_factory=lambda: list(range(96)))   # regressors: all 96 factors
+    ycol: int = TARGET                                             # next-day excess return
+    train_frac: float = 0.6        # dates [0, train) train, [train, test) valid, [test, T) test
+    valid_frac: float = 0.2
+    top_n: int = 10                # KKT:796
+    window: int = 252              # rolling covariance window (north star); None = whole history
+    lo: float = 0.0                # KKT:828
+    hi: float = 0.1
+    rate: float = 1e-4             # KKT:796
+    tol: float = 1e-10
+
+
+class Pipeline:
+    def __init__(self, grid: PanelGrid, cfg: PipelineConfig | None = None):
+        import torch
+        self.g = grid
+        self.cfg = cfg or PipelineConfig()
+        dev = grid.device
+        T, lda = grid.T, grid.lda
+        nch = (T + 63) // 64
+        self.T, self.lda, self.p = T, lda, len(self.cfg.cols)
+        self.t_valid = int(T * self.cfg.train_frac)
+        self.t_test = int(T * (self.cfg.train_frac + self.cfg.valid_frac))
+        p2 = self.p + 2
+        f64 = dict(dtype=torch.float64, device=dev)
+        i64 = dict(dtype=torch.int64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.out = torch.empty((N_FACTORS, T, lda), **f64)
+        self.nanfree = torch.zeros((nch, lda), **i64)
+        self.finite = torch.zeros((nch, lda), **i64)
+        self.cols = torch.as_tensor(np.asarray(self.cfg.cols, dtype=np.int32), device=dev)
+        self.gram = torch.empty((T, p2, p2), **f64)
+        self.shift = torch.empty((T, p2), **f64)
+        self.beta = torch.empty((T, self.p + 1), **f64)
+        self.nobs = torch.empty(T, **f64)
+        self.rank = torch.empty(T, **i32)
+        self.fm_mean = torch.empty(self.p + 1, **f64)
+        self.fm_t = torch.empty(self.p + 1, **f64)
+        self.pool_g = torch.empty((1, p2, p2), **f64)
+        self.pool_s = torch.empty((1, p2), **f64)
+        self.pool_beta = torch.empty((1, self.p + 1), **f64)
+        self.pool_n = torch.empty(1, **f64)
+        self.pool_rank = torch.empty(1, **i32)
+        self.pred = torch.full((T, lda), float("nan"), **f64)
+        # rebalance dates: the test dates (the last calendar date carries no label -> no rows)
+        rd = np.arange(self.t_test, T - 1, dtype=np.int32)
+        self.rdates = torch.from_numpy(rd).to(dev)
+        nd = len(rd)
+        self.nd = nd
+        self.reb = {
+            "k": torch.empty(nd, **i32),
+            "books": torch.full((nd, 2, MAX_BOOK), -1, **i32),
+            "weights": torch.zeros((nd, 2, MAX_BOOK), **f64),
+            "sums": torch.empty((nd, 4), **f64),
+            "upos": torch.empty((nd, 2, 2, MAX_BOOK), **i32),
+            "usize": torch.empty((nd, 2), **i64),
+            "status": torch.empty(nd, **i32),
+        }
+        self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
+                    "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
+        self.ctx = _lib.Context.get(dev.index)
+
+    def step(self, events: dict | None = None):
+        """One pass of the hot path.  ``events``: optional {stage: (start, end)} CUDA events."""
+        L = _lib.lib()
+        P = _lib.ptr
+        chk = _lib.check
+        g, c = self.g, self.cfg
+        T, lda, p = self.T, self.lda, self.p
+        h = self.ctx.bind_stream()
+
+        def mark(stage, which):
+            if events is not None:
+                events[stage][which].record()
+
+        mark("factors", 0)
+        chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), P(g.ret1d), P(g.excess),
+                              P(g.vbits), P(self.out), P(self.nanfree), P(self.finite)), "factors")
+        mark("factors", 1)
+        mark("xs_gram", 0)
+        chk(L.afm_xs_gram_f64(h, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p, c.ycol,
+                              P(self.finite), 0, T, P(self.gram), P(self.shift)), "xs_gram")
+        mark("xs_gram", 1)
+        mark("xs_solve", 0)
+        chk(L.afm_ols_solve_f64(h, P(self.gram), P(self.shift), p, T, c.tol, P(self.beta),
+                                P(self.nobs), P(self.rank)), "ols_solve")
+        chk(L.afm_fama_macbeth_f64(h, P(self.beta), P(self.rank), T, p + 1, P(self.fm_mean),
+                                   P(self.fm_t)), "fama_macbeth")
+        mark("xs_solve", 1)
+        mark("pooled_ols", 0)
+        chk(L.afm_pool_moments_f64(h, P(self.gram), P(self.shift), p, self.t_test,
+                                   P(self.pool_g), P(self.pool_s)), "pool")
+        chk(L.afm_ols_solve_f64(h, P(self.pool_g), P(self.pool_s), p, 1, c.tol,
+                                P(self.pool_beta), P(self.pool_n), P(self.pool_rank)), "pool_solve")
+        mark("pooled_ols", 1)
+        mark("predict", 0)
+        chk(L.afm_predict_f64(h, P(self.out), T * lda, lda, self.t_test, T - self.t_test,
+                              P(self.cols), p, P(self.pool_beta), 0, P(self.finite), c.ycol,
+                              P(self.pred)), "predict")
+        mark("predict", 1)
+        mark("rebalance", 0)
+        r = self.reb
+        chk(L.afm_rebalance_f64(h, T, g.A, lda, P(self.rdates), self.nd, P(self.pred),
+                                P(g.tbits), P(self.out[c.ycol]), P(g.vbits), 0, T,
+                                -1 if c.window is None else int(c.window), P(g.close),
+                                P(self.out[N_FACTORS - 1]), c.top_n, c.lo, c.hi, P(r["k"]),
+                                P(r["books"]), P(r["weights"]), P(r["sums"]), P(r["upos"]),
+                                P(r["usize"]), P(r["status"])), "rebalance")
+        mark("rebalance", 1)
+        mark("pnl", 0)
+        q = self.pnl
+        chk(L.afm_pnl_scan_f64(h, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]), P(r["upos"]),
+                               P(r["usize"]), 100000000.0, c.rate, P(q["value"]),
+                               P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])), "pnl")
+        mark("pnl", 1)
+
+    def summary(self) -> dict:
+        """Host copies of the headline results (after a synchronize)."""
+        v = self.pnl["value"].cpu().numpy()
+        r = v[1:] / v[:-1] - 1
+        return {"final_value": float(v[-1]), "sharpe": float(r.mean() / r.std(ddof=1)),
+                "fm_mean": self.fm_mean.cpu().numpy(), "fm_t": self.fm_t.cpu().numpy(),
+                "pooled_beta": self.pool_beta[0].cpu().numpy(),
+                "ranks": self.rank.cpu().numpy(), "k": self.reb["k"].cpu().numpy(),
+                "status": self.reb["status"].cpu().numpy()}

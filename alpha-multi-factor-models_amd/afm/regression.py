@@ -87,7 +87,7 @@ def fama_macbeth(beta, rank):
 
 
 def predict_grid(planes, lda: int, cols, beta, bits, t0: int, nt: int, per_date: bool = False,
-                 out=None):
+                 out=None, ycheck: int = -1):
     """pred[t][a] = beta0 + sum_j beta_j x_j for grid rows with a mask bit (NaN elsewhere)."""
     import torch
     dev = planes.device
@@ -100,7 +100,8 @@ def predict_grid(planes, lda: int, cols, beta, bits, t0: int, nt: int, per_date:
     stride = beta.shape[-1] if per_date else 0
     _lib.check(_lib.lib().afm_predict_f64(ctx.bind_stream(), P(planes), T * lda, lda, t0, nt,
                                           P(cols_t), int(cols_t.numel()), P(beta.contiguous()),
-                                          stride, P(bits), P(out)), "afm_predict_f64")
+                                          stride, P(bits), int(ycheck), P(out)),
+               "afm_predict_f64")
     return out
 
 

@@ -49,6 +49,7 @@ struct Smem {
     double c[kRing][kLanes];   // close ring (by observation index mod kRing)
     double v[kRing][kLanes];   // volume ring
     u64 nanmask[kLanes];
+    u64 badmask[kLanes];       // some factor non-finite (NaN or +-inf)
 };
 
 struct Args {
@@ -58,6 +59,7 @@ struct Args {
     const uint64_t* vbits;
     double* out;
     uint64_t* nanfree;
+    uint64_t* finite;          // optional
 };
 
 // Per-lane view of one (asset, present day) step.
@@ -66,12 +68,13 @@ struct Step {
     double* out;
     int64_t plane, cell;
     int lane, p;               // p = index of this observation in the asset's series
-    bool anynan;
+    bool anynan, anybad;
     __device__ __forceinline__ double C(int q) const { return sm->c[q & (kRing - 1)][lane]; }
     __device__ __forceinline__ double V(int q) const { return sm->v[q & (kRing - 1)][lane]; }
     __device__ __forceinline__ void put(int col, double x) {
         out[col * plane + cell] = x;
         anynan |= (x != x);
+        anybad |= !__builtin_isfinite(x);
     }
     // close.pct_change() at q, with the window kernels' inf -> NaN (_prep_values)
     __device__ __forceinline__ double ret(int q) const {
@@ -506,7 +509,10 @@ __device__ __noinline__ void run_wave(const Args& a, Smem& sm, int wave, int lan
                 sm.v[q & (kRing - 1)][lane] = pv[j];
             }
         }
-        if (wave == 0) sm.nanmask[lane] = 0ull;
+        if (wave == 0) {
+            sm.nanmask[lane] = 0ull;
+            sm.badmask[lane] = 0ull;
+        }
         // prefetch the next chunk while this one is scanned
         if (ch + 1 < nch) {
             vb_next = a.vbits[(int64_t)(ch + 1) * a.lda + asset];
@@ -522,7 +528,7 @@ __device__ __noinline__ void run_wave(const Args& a, Smem& sm, int wave, int lan
 
         const int64_t t0 = (int64_t)ch * kChunk;
         const int steps = (int)min((int64_t)kChunk, a.T - t0);
-        u64 nb = 0ull;
+        u64 nb = 0ull, fb = 0ull;
         int p = pos;
         for (int s = 0; s < steps; ++s) {
             if ((vb >> s) & 1ull) {
@@ -534,14 +540,20 @@ __device__ __noinline__ void run_wave(const Args& a, Smem& sm, int wave, int lan
                 st.lane = lane;
                 st.p = p;
                 st.anynan = false;
+                st.anybad = false;
                 jobs.step(st);
                 if (st.anynan) nb |= 1ull << s;
+                if (st.anybad) fb |= 1ull << s;
                 ++p;
             }
         }
         if (nb) atomicOr(&sm.nanmask[lane], nb);
+        if (fb) atomicOr(&sm.badmask[lane], fb);
         __syncthreads();
-        if (wave == 0) a.nanfree[(int64_t)ch * a.lda + asset] = vb & ~sm.nanmask[lane];
+        if (wave == 0) {
+            a.nanfree[(int64_t)ch * a.lda + asset] = vb & ~sm.nanmask[lane];
+            if (a.finite) a.finite[(int64_t)ch * a.lda + asset] = vb & ~sm.badmask[lane];
+        }
         pos = p;
     }
 }
@@ -610,7 +622,7 @@ __global__ __launch_bounds__(256) void labels_kernel(int64_t T, int64_t lda, con
 extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                                const double* close, const double* volume, const double* ret1d,
                                const double* excess, const uint64_t* valid_bits, double* out,
-                               uint64_t* nanfree_bits) {
+                               uint64_t* nanfree_bits, uint64_t* finite_bits) {
     AFM_CTX(ctx);
     AFM_CHECK_ARG(T > 0 && A > 0, "T and A must be positive");
     AFM_CHECK_ARG(lda >= A && lda % 64 == 0, "lda must be a multiple of 64 and >= A");
@@ -626,6 +638,7 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     a.vbits = valid_bits;
     a.out = out;
     a.nanfree = nanfree_bits;
+    a.finite = finite_bits;
     dim3 grid((unsigned)(lda / 64));
     hipLaunchKernelGGL(afm::factor_panel_kernel, grid, dim3(64 * 16), 0, ctx->stream, a);
     AFM_HIP(hipGetLastError());

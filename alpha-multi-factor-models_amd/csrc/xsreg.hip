@@ -351,14 +351,17 @@ __global__ __launch_bounds__(256) void predict_kernel(const double* base, int64_
                                                       int64_t lda, int64_t t0, int64_t nt,
                                                       const int32_t* cols, int p,
                                                       const double* beta, int64_t beta_stride,
-                                                      const uint64_t* bits, double* pred) {
+                                                      const uint64_t* bits, int ycheck,
+                                                      double* pred) {
     const int64_t a = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const int64_t t = t0 + (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
     if (t >= t0 + nt) return;
     const double* b = beta + (t - t0) * beta_stride;
     u64 w = bits[(t >> 6) * lda + a];
     double v = __builtin_nan("");
-    if ((w >> (t & 63)) & 1ull) {
+    bool use = (w >> (t & 63)) & 1ull;
+    if (use && ycheck >= 0) use = __builtin_isfinite(base[(int64_t)ycheck * col_stride + t * lda + a]);
+    if (use) {
         double s = b[0];
         for (int j = 0; j < p; ++j) s = s + b[1 + j] * base[(int64_t)cols[j] * col_stride + t * lda + a];
         v = s;
@@ -434,14 +437,14 @@ extern "C" int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const doub
 extern "C" int afm_predict_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
                                int64_t t0, int64_t nt, const int32_t* cols, int p,
                                const double* beta, int64_t beta_stride, const uint64_t* bits,
-                               double* pred) {
+                               int ycheck, double* pred) {
     AFM_CTX(ctx);
     AFM_CHECK_ARG(base && cols && beta && bits && pred, "null buffer");
     AFM_CHECK_ARG(lda % 64 == 0 && nt >= 0 && t0 >= 0, "bad shape");
     if (nt == 0) return AFM_OK;
     dim3 grid((unsigned)(lda / 64), (unsigned)((nt + 3) / 4));
     hipLaunchKernelGGL(predict_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride, lda, t0,
-                       nt, cols, p, beta, beta_stride, bits, pred);
+                       nt, cols, p, beta, beta_stride, bits, ycheck, pred);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

@@ -1,12 +1,17 @@
 #!/usr/bin/env python3
-"""Headline benchmark: asset-days/s for the factor-research hot path (BASELINE.json ``metric``).
+"""Headline benchmark: asset-days/s for factor build + cross-sectional regression + KKT weights
+(BASELINE.json ``metric``), SURVEY.md §8(d).
 
 Workload (N=1): BASELINE.json configs[2] -- 10,000 assets x 20 years (5,040 trading days) daily
-synthetic panel (seeded generator of SURVEY.md §8(d), ragged listings, 0.2% holes), inputs
-resident in HBM before the timed region.  One step = one pass of the hot path over the panel.
+synthetic panel (seeded generator, SURVEY.md §8(d): ragged listings, 0.2% holes), inputs
+resident in HBM before the timed region.  One step = afm.pipeline.Pipeline.step(): 98-column
+factor build, per-date OLS of next-day excess return on all 96 factors (fp64 MFMA Grams) + FM
+stats, pooled OLS over the train+valid dates, predictions on the test dates (last 20%),
+rolling-252-day covariance + exact min-variance KKT weights for top/bottom-10 books on every
+test date, PnL/turnover scan.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; for N>1 the driver launches it with
-torch.distributed.run (one rank per GPU).  Rank 0 prints ONE JSON line.
+Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 is launched by torch.distributed.run
+(one rank per GPU).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -20,7 +25,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "alpha-multi-factor-models_amd"))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md chip table)
+F64_MFMA_PEAK_TFS = 78.6       # MI355X fp64 matrix peak (spec)
 FACTOR_BYTES_PER_AD = 816      # 4 x 8 B inputs read + 98 x 8 B outputs written
 
 
@@ -28,30 +34,49 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(seed: int):
-    """The oracle (C restatement of No-talib.py, 1 thread) on a bounded sample: config A
-    (500 assets x 2,520 days)."""
+def cpu_baseline(seed: int, assets: int = 500, days: int = 2520):
+    """The oracle chain (C factor restatement + numpy per-date lstsq + sklearn pooled OLS +
+    numpy/Python portfolio with the exact QP), 1 core, on config A (500 assets x 2520 days)."""
     import numpy as np
+    from threadpoolctl import threadpool_limits
 
     import oracle
+    from oracle import pipeline as PL
+    from oracle import portfolio as PF
     from afm.synthetic import make_panel
-    p = make_panel(500, 2520, seed=seed)
+    p = make_panel(assets, days, seed=seed)
     v = p.valid[:, :p.A]
     aa, tt = np.nonzero(v.T)
     off = np.r_[0, np.cumsum(v.sum(axis=0))].astype(np.int64)
     cols = [np.ascontiguousarray(x[tt, aa]) for x in (p.close, p.volume, p.ret1d, p.excess)]
-    oracle.factors_long(off[:3], *[c[: off[2]] for c in cols])      # warm the library
+    n_ad = len(tt)
+    limiter = threadpool_limits(1)                                       # 1 core, BLAS included
     t0 = time.perf_counter()
-    reps = 0
-    while True:
-        oracle.factors_long(off, *cols)
-        reps += 1
-        if time.perf_counter() - t0 > 10.0 or reps >= 20:
-            break
-    dt = (time.perf_counter() - t0) / reps
-    return {"value": round(len(tt) / dt, 1), "unit": "asset-days/s", "cores": 1, "kind": "port",
-            "sample": f"factor build (oracle/factors_oracle.c, No-talib.py restated) on config A "
-                      f"500 assets x 2520 days = {len(tt)} asset-days, {reps} reps"}
+    fac = oracle.factors_long(off, *cols)                               # factors
+    t1 = time.perf_counter()
+    X, y = fac[:, :96], fac[:, 96]
+    use = np.isfinite(X).all(axis=1) & np.isfinite(y)
+    T = days
+    t_test = int(T * 0.8)
+    PL.xs_ols(tt[use], X[use], y[use])                                   # per-date OLS
+    t2 = time.perf_counter()
+    tv = use & (tt < t_test)
+    b0, b = PL.pooled_ols(X[tv], y[tv])                                  # pooled OLS
+    te = use & (tt >= t_test) & (tt < T - 1)
+    pred = b0 + X[te] @ b
+    t3 = time.perf_counter()
+    ids = p.ids[aa]
+    dates = p.dates[tt].astype(np.int64)
+    trad = p.tradable[tt, aa]
+    PF.run_portfolio(dates[te], ids[te], pred, dates, ids, y, dates, ids, trad,   # KKT stage
+                     cols[0], fac[:, 97], window=252)
+    t4 = time.perf_counter()
+    limiter.unregister() if hasattr(limiter, "unregister") else None
+    total = t4 - t0
+    return {"value": round(n_ad / total, 1), "unit": "asset-days/s", "cores": 1, "kind": "port",
+            "sample": f"oracle chain on config A ({assets} assets x {days} days = {n_ad} "
+                      f"asset-days): factors {t1 - t0:.2f}s, per-date OLS {t2 - t1:.2f}s, pooled "
+                      f"OLS+predict {t3 - t2:.2f}s, rebalance+KKT+PnL {t4 - t3:.2f}s"}
 
 
 def main():
@@ -70,6 +95,7 @@ def main():
     import torch.distributed as dist
 
     import afm
+    from afm.pipeline import STAGES, Pipeline
     from afm.synthetic import make_panel
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -80,13 +106,13 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    # ---- synthetic panel (identical on every rank), asset shard of this rank -------------------
     t0 = time.perf_counter()
     p = make_panel(args.assets, args.days, seed=args.seed)
-    lo = (args.assets * rank) // world
-    hi = (args.assets * (rank + 1)) // world
     if world > 1:
+        # interim multi-GPU mode: each rank runs the full pipeline on its slice of assets
         from afm.synthetic import Panel, round_up
+        lo = (args.assets * rank) // world
+        hi = (args.assets * (rank + 1)) // world
         lda = round_up(hi - lo)
 
         def sl(x, fill):
@@ -100,36 +126,33 @@ def main():
     grid = afm.PanelGrid.from_panel(p, device=dev)
     del p
     n_ad = grid.n_asset_days()
-    out = torch.empty((afm.factors.N_FACTORS, grid.T, grid.lda), dtype=torch.float64, device=dev)
-    nanfree = torch.zeros(((grid.T + 63) // 64, grid.lda), dtype=torch.int64, device=dev)
+    pipe = Pipeline(grid)
     torch.cuda.synchronize()
     log(f"[rank {rank}] panel {grid.A}x{grid.T} ({n_ad} asset-days) ready in "
         f"{time.perf_counter() - t0:.1f}s")
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record()
-        afm.factor_panel(grid, out, nanfree)
-        if ev is not None:
-            ev[1].record()
-
     for _ in range(args.warmup):
-        step()
+        pipe.step()
     torch.cuda.synchronize()
+    if rank == 0 and args.warmup:
+        s = pipe.summary()
+        log(f"[rank 0] warmup: final value {s['final_value']:.6g}, sharpe {s['sharpe']:.4g}, "
+            f"per-date ranks {np.bincount(s['ranks'])[-3:]}, qp status {np.bincount(s['status'])}")
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    evs = [{st: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for st in STAGES} for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        pipe.step(evs[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    fac_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    stage_ms = {st: sum(e[st][0].elapsed_time(e[st][1]) for e in evs) / args.steps
+                for st in STAGES}
 
     total_ad = n_ad
     if world > 1:
@@ -143,7 +166,21 @@ def main():
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        achieved = FACTOR_BYTES_PER_AD * n_ad / (fac_ms * 1e-3) / 1e9
+        # roofline of the dominant kernel: factor panel (HBM) or the per-date Gram (fp64 MFMA)
+        p = pipe.p
+        fac_gbs = FACTOR_BYTES_PER_AD * n_ad / (stage_ms["factors"] * 1e-3) / 1e9
+        gram_rows = float(pipe.nobs.sum().item())
+        gram_tfs = gram_rows * (p + 2) * (p + 3) / (stage_ms["xs_gram"] * 1e-3) / 1e12
+        if stage_ms["factors"] >= stage_ms["xs_gram"]:
+            roof = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(fac_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "factor_panel_kernel+labels_kernel",
+                    "kernel_ms": round(stage_ms["factors"], 3)}
+        else:
+            roof = {"bound": "mfma", "achieved": round(gram_tfs, 2), "peak": F64_MFMA_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": round(gram_tfs / F64_MFMA_PEAK_TFS, 4),
+                    "traffic": None, "kernel": "gram_kernel",
+                    "kernel_ms": round(stage_ms["xs_gram"], 3)}
         res = {
             "metric": "asset-days/sec, factor build+XS regression+KKT (10k assets x 20y), "
                       "1/2/4/8 GPU",
@@ -153,14 +190,15 @@ def main():
             "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (seeded OHLCV panel, SURVEY.md §8(d))",
-            "config": {"workload": f"factor build (98 cols, No-talib.py) on {args.assets} assets x "
-                                   f"{args.days} days; stages: factors",
+            "config": {"workload": f"{args.assets} assets x {args.days} days daily panel: 98 "
+                                   f"factors -> per-date OLS on 96 factors + FM -> pooled OLS -> "
+                                   f"predict -> rolling-252 cov + exact KKT top/bottom-10 -> PnL",
                        "assets": args.assets, "days": args.days, "asset_days": total_ad,
                        "parallelism": f"asset-shard x{world}" if world > 1 else "single"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "factor_panel_kernel+labels_kernel",
-                         "kernel_ms": round(fac_ms, 3)},
+            "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
+            "roofline": roof,
+            "secondary": {"factor_panel_GBps": round(fac_gbs, 1),
+                          "gram_TFLOPs": round(gram_tfs, 2)},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.seed)

@@ -51,11 +51,13 @@ const char* afm_factor_name(int i);
  * out: [AFM_N_FACTORS][T][lda]; cells of absent asset-days are left untouched.
  * nanfree_bits [ceil(T/64)][lda]: present AND all 96 factor columns non-NaN (target/tmr_ret1d
  * excluded: their NaN-ness is read from their planes), i.e. the dropna() row mask of
- * No-talib.py:33 before the pass-through and label columns are considered. */
+ * No-talib.py:33 before the pass-through and label columns are considered.
+ * finite_bits (optional, may be NULL): present AND all 96 factor columns finite (dropna keeps
+ * +-inf, e.g. vol_change after a zero-volume day; the regression stages need finite rows). */
 int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                     const double* close, const double* volume, const double* ret1d,
                     const double* excess, const uint64_t* valid_bits,
-                    double* out, uint64_t* nanfree_bits);
+                    double* out, uint64_t* nanfree_bits, uint64_t* finite_bits);
 
 /* ---- R1: cross-sectional regression ---------------------------------------------------------
  * Segmented shifted Gram on fp64 MFMA.  Segment t (t = seg0 .. seg0+nseg-1) is the rows
@@ -78,10 +80,11 @@ int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double* shift, int
 int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
                          int64_t nseg, double* out_gram, double* out_shift);
 /* pred[t][a] = beta[t-t0][0] + sum_j beta[t-t0][1+j] * x_cols[j][t][a] on grid rows with a mask
- * bit (NaN elsewhere), t in [t0, t0+nt); beta_stride = 0 applies one coefficient vector. */
+ * bit (NaN elsewhere), t in [t0, t0+nt); beta_stride = 0 applies one coefficient vector.
+ * ycheck >= 0: additionally require column ycheck finite (e.g. the label of a dropna'd row). */
 int afm_predict_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda, int64_t t0,
                     int64_t nt, const int32_t* cols, int p, const double* beta,
-                    int64_t beta_stride, const uint64_t* bits, double* pred);
+                    int64_t beta_stride, const uint64_t* bits, int ycheck, double* pred);
 /* Fama-MacBeth over segments with rank > 0: mean_t beta_t and mean / (std / sqrt(T)). */
 int afm_fama_macbeth_f64(afm_ctx* ctx, const double* beta, const int32_t* rank, int64_t nseg,
                          int k, double* mean_out, double* t_out);

@@ -65,6 +65,6 @@ def test_factor_kernel_rejects_bad_shapes():
     p = make_panel(10, 100, seed=0)
     grid = afm.PanelGrid.from_panel(p)
     ctx = _lib.Context.get()
-    rc = _lib.lib().afm_factors_f64(ctx.bind_stream(), 100, 10, 60, *([None] * 7))
+    rc = _lib.lib().afm_factors_f64(ctx.bind_stream(), 100, 10, 60, *([None] * 8))
     assert rc != 0 and b"lda" in _lib.lib().afm_last_error()
     torch.cuda.synchronize()
