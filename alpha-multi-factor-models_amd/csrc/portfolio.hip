@@ -559,86 +559,111 @@ __device__ double pairwise_sparse(const int64_t* pos, const double* val, int m, 
            pairwise_sparse(pos, val, m, lo + n2, n - n2, depth + 1);
 }
 
-__global__ void pnl_scan_kernel(int64_t nd, const int32_t* k_out, const int32_t* books,
-                                const double* sums, const int32_t* upos, const int64_t* usize,
-                                double v0, double rate, double* value, double* turnover,
-                                double* long_ret, double* short_ret) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double V = v0;
-    value[0] = V;
-    // positions of the previous date's members
-    int64_t pos_buf[4 * kMaxK];
-    double val_buf[4 * kMaxK];
+// Turnover terms of date i >= 1 (structure only; the values need V): for each id in the previous
+// or current books that is predicted on both dates, its union position and its side on each date
+// (0 long, 1 short, 2 none).  Sorted by union position.  One 64-thread block per date.
+constexpr int kMaxTerms = 4 * kMaxK;
+
+__global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const int32_t* k_out,
+                                                            const int32_t* books,
+                                                            const int32_t* upos, int32_t* tpos,
+                                                            int32_t* tside, int32_t* tcount) {
+    __shared__ int pos_s[kMaxTerms], side_s[kMaxTerms];
+    __shared__ int cnt;
+    const int64_t i = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    if (i > 0 && k_out[i - 1] > 0) {          // current_positions.dropna().empty -> 0 (KKT:836)
+        const int k = k_out[i], kp = k_out[i - 1];
+        // previous members predicted today
+        for (int e = tid; e < 2 * kp; e += 64) {
+            const int side = e / kp, q = e % kp;
+            const int a = books[((i - 1) * 2 + side) * kMaxK + q];
+            const int pz = upos[(((i - 1) * 2 + side) * 2 + 1) * kMaxK + q];
+            if (pz < 0) continue;
+            int ns = 2;
+            for (int s2 = 0; s2 < 2; ++s2)
+                for (int q2 = 0; q2 < k; ++q2)
+                    if (books[(i * 2 + s2) * kMaxK + q2] == a) ns = s2;
+            const int slot = atomicAdd(&cnt, 1);
+            pos_s[slot] = pz;
+            side_s[slot] = side * 3 + ns;
+        }
+        // current members predicted yesterday and not in yesterday's books
+        for (int e = tid; e < 2 * k; e += 64) {
+            const int side = e / k, q = e % k;
+            const int a = books[(i * 2 + side) * kMaxK + q];
+            const int pz = upos[((i * 2 + side) * 2 + 0) * kMaxK + q];
+            if (pz < 0) continue;
+            bool inprev = false;
+            for (int s2 = 0; s2 < 2; ++s2)
+                for (int q2 = 0; q2 < kp; ++q2)
+                    if (books[((i - 1) * 2 + s2) * kMaxK + q2] == a) inprev = true;
+            if (inprev) continue;
+            const int slot = atomicAdd(&cnt, 1);
+            pos_s[slot] = pz;
+            side_s[slot] = 2 * 3 + side;
+        }
+    }
+    __syncthreads();
+    const int m = cnt;
+    for (int e = tid; e < m; e += 64) {       // rank by count (positions are distinct)
+        int r = 0;
+        for (int f = 0; f < m; ++f) r += pos_s[f] < pos_s[e];
+        tpos[i * kMaxTerms + r] = pos_s[e];
+        tside[i * kMaxTerms + r] = side_s[e];
+    }
+    if (tid == 0) tcount[i] = i > 0 && k_out[i - 1] > 0 ? m : -1;
+}
+
+// The value recursion (KKT:864-892).  Per date the term values |c - n| are formed in parallel
+// (c, n = +-(V/2)/den exactly as the reference computes them), the turnover is numpy's pairwise
+// sum over the aligned union vector evaluated at the terms' positions, then V advances.
+__global__ __launch_bounds__(64) void pnl_scan_kernel(int64_t nd, const double* sums,
+                                                      const int32_t* tpos, const int32_t* tside,
+                                                      const int32_t* tcount, const int64_t* usize,
+                                                      double v0, double rate, double* value,
+                                                      double* turnover, double* long_ret,
+                                                      double* short_ret) {
+    __shared__ int64_t pos_s[kMaxTerms];
+    __shared__ double val_s[kMaxTerms];
+    __shared__ double Vs;
+    const int tid = threadIdx.x;
+    if (tid == 0) { Vs = v0; value[0] = v0; }
+    __syncthreads();
     for (int64_t i = 0; i < nd; ++i) {
-        const int k = k_out[i];
+        const double V = Vs;
         const double* sm = sums + i * 4;
-        const double size = V / 2;
-        double daily = (sm[0] - sm[1]) / 2;
-        long_ret[i] = sm[0];
-        short_ret[i] = sm[1];
-        double to = 0.0;
-        if (i > 0 && k_out[i - 1] > 0) {   // current_positions.dropna().empty -> 0 (KKT:836-837)
-            const int kp = k_out[i - 1];
+        const int m = tcount[i];
+        if (m > 0) {
             const double* sp = sums + (i - 1) * 4;
             const double Vp = value[i - 1];
-            const double sizep = Vp / 2;
-            int m = 0;
-            // members of the previous books that are predicted today: |c - n|
-            for (int side = 0; side < 2; ++side) {
-                for (int q = 0; q < kp; ++q) {
-                    const int a = books[((i - 1) * 2 + side) * kMaxK + q];
-                    const int pz = upos[(((i - 1) * 2 + side) * 2 + 1) * kMaxK + q];
-                    if (pz < 0) continue;
-                    double c = side == 0 ? sizep / sp[2] : -sizep / sp[3];
-                    double nv = 0.0;
-                    for (int s2 = 0; s2 < 2; ++s2)
-                        for (int q2 = 0; q2 < k; ++q2)
-                            if (books[(i * 2 + s2) * kMaxK + q2] == a)
-                                nv = s2 == 0 ? size / sm[2] : -size / sm[3];
-                    pos_buf[m] = pz;
-                    double d = c - nv;
-                    val_buf[m] = d < 0 ? -d : d;
-                    ++m;
-                }
+            const double sizep = Vp / 2, size = V / 2;
+            for (int e = tid; e < m; e += 64) {
+                const int sd = tside[i * kMaxTerms + e];
+                const int ps = sd / 3, ns = sd % 3;
+                const double c = ps == 0 ? sizep / sp[2] : (ps == 1 ? -sizep / sp[3] : 0.0);
+                const double n = ns == 0 ? size / sm[2] : (ns == 1 ? -size / sm[3] : 0.0);
+                const double d = c - n;
+                val_s[e] = d < 0 ? -d : d;
+                pos_s[e] = tpos[i * kMaxTerms + e];
             }
-            // members of today's books that were predicted yesterday but not in its books
-            for (int side = 0; side < 2; ++side) {
-                for (int q = 0; q < k; ++q) {
-                    const int a = books[(i * 2 + side) * kMaxK + q];
-                    const int pz = upos[((i * 2 + side) * 2 + 0) * kMaxK + q];
-                    if (pz < 0) continue;
-                    bool inprev = false;
-                    for (int s2 = 0; s2 < 2; ++s2)
-                        for (int q2 = 0; q2 < kp; ++q2)
-                            if (books[((i - 1) * 2 + s2) * kMaxK + q2] == a) inprev = true;
-                    if (inprev) continue;
-                    double nv = side == 0 ? size / sm[2] : -size / sm[3];
-                    double d = 0.0 - nv;
-                    pos_buf[m] = pz;
-                    val_buf[m] = d < 0 ? -d : d;
-                    ++m;
-                }
-            }
-            // sort by union position (insertion sort, m <= 4 kMaxK)
-            for (int a = 1; a < m; ++a) {
-                int64_t pk = pos_buf[a];
-                double pv = val_buf[a];
-                int b = a - 1;
-                while (b >= 0 && pos_buf[b] > pk) {
-                    pos_buf[b + 1] = pos_buf[b];
-                    val_buf[b + 1] = val_buf[b];
-                    --b;
-                }
-                pos_buf[b + 1] = pk;
-                val_buf[b + 1] = pv;
-            }
-            to = pairwise_sparse(pos_buf, val_buf, m, 0, usize[i * 2 + 0], 0) / 2;
         }
-        turnover[i] = to;
-        const double cost = to * rate;
-        daily -= cost / V;
-        V = V * (1 + daily);
-        value[i + 1] = V;
+        __syncthreads();
+        if (tid == 0) {
+            double daily = (sm[0] - sm[1]) / 2;
+            long_ret[i] = sm[0];
+            short_ret[i] = sm[1];
+            double to = 0.0;
+            if (m > 0) to = pairwise_sparse(pos_s, val_s, m, 0, usize[i * 2 + 0], 0) / 2;
+            turnover[i] = to;
+            daily -= (to * rate) / V;
+            const double Vn = V * (1 + daily);
+            value[i + 1] = Vn;
+            Vs = Vn;
+        }
+        __syncthreads();
     }
 }
 
@@ -681,9 +706,19 @@ extern "C" int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out,
     AFM_CHECK_ARG(k_out && books && sums && upos && usize && value && turnover && long_ret &&
                       short_ret, "null buffer");
     if (nd <= 0) return AFM_OK;
-    hipLaunchKernelGGL(pnl_scan_kernel, dim3(1), dim3(64), 0, ctx->stream, nd, k_out, books,
-                       sums, upos, usize, v0, rate, value, turnover, long_ret, short_ret);
+    int32_t* work = nullptr;
+    const size_t words = (size_t)nd * (2 * kMaxTerms + 1);
+    AFM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * words, ctx->stream));
+    int32_t* tpos = work;
+    int32_t* tside = work + nd * kMaxTerms;
+    int32_t* tcount = work + 2 * nd * kMaxTerms;
+    hipLaunchKernelGGL(turnover_terms_kernel, dim3((unsigned)nd), dim3(64), 0, ctx->stream, nd,
+                       k_out, books, upos, tpos, tside, tcount);
     AFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(pnl_scan_kernel, dim3(1), dim3(64), 0, ctx->stream, nd, sums, tpos, tside,
+                       tcount, usize, v0, rate, value, turnover, long_ret, short_ret);
+    AFM_HIP(hipGetLastError());
+    AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;
 }
 

@@ -57,9 +57,12 @@ __device__ __forceinline__ int pair_J(int q, int nt) {
     return I + q;
 }
 
+constexpr int kPer = ((kMaxF - 1) * kRows + kThreads - 1) / kThreads;   // staged values per thread
+
 __global__ __launch_bounds__(kThreads) void gram_kernel(GramArgs g) {
     __shared__ double tile[kMaxF][kRS];
     __shared__ double sh[kMaxF];
+    __shared__ int colsL[kMaxF];
     __shared__ int rowok[kRows];
     __shared__ int flags[2];               // [0] shift set, [1] tile has a usable row
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -72,17 +75,46 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(GramArgs g) {
     const int wp = wave % WP, wk = wave / WP;
     const int64_t seg = g.seg0 + blockIdx.x;
     const int64_t rowbase = seg * g.seg_stride;
+    const int nstage = (p + 1) * kRows;
 
     for (int i = tid; i < kMaxF * kRS; i += kThreads) (&tile[0][0])[i] = 0.0;
     if (tid < kMaxF) sh[tid] = 0.0;
+    if (tid < p + 1) colsL[tid] = tid < p ? g.cols[tid] : g.ycol;
     if (tid == 0) flags[0] = 0;
+    // this wave's tile pairs
+    int pI[kMaxTiles], pJ[kMaxTiles];
+#pragma unroll
+    for (int q = 0; q < kMaxTiles; ++q) {
+        const int pq = wp + q * WP;
+        pI[q] = pq < npairs ? pair_I(pq, nt) : 0;
+        pJ[q] = pq < npairs ? pair_J(pq, nt) : 0;
+    }
     d4 acc[kMaxTiles];
 #pragma unroll
     for (int q = 0; q < kMaxTiles; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
     __syncthreads();
 
+    // register prefetch of one 64-row tile of features 1..p+1
+    double pre[kPer];
+    auto prefetch = [&](int64_t r0) {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = tid + j * kThreads;
+            double x = 0.0;
+            if (i < nstage) {
+                const int f = 1 + (i >> 6), a = i & (kRows - 1);
+                const int64_t r = r0 + a;
+                bool in = r < g.seg_rows;
+                if (g.row_limit >= 0) in = in && (rowbase + r < g.row_limit);
+                if (in) x = g.base[(int64_t)colsL[f - 1] * g.col_stride + rowbase + r];
+            }
+            pre[j] = x;
+        }
+    };
+    prefetch(0);
+
     for (int64_t r0 = 0; r0 < g.seg_rows; r0 += kRows) {
-        // ---- stage rows r0..r0+63 of features 1..p+1 ----
+        // ---- row mask of rows r0..r0+63, stage the prefetched values ----
         if (tid < kRows) {
             int64_t r = r0 + tid;
             bool ok = r < g.seg_rows;
@@ -94,17 +126,18 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(GramArgs g) {
             rowok[tid] = ok ? 1 : 0;
         }
         __syncthreads();
-        for (int i = tid; i < (p + 1) * kRows; i += kThreads) {
-            int f = 1 + i / kRows, a = i % kRows;
-            double x = 0.0;
-            if (rowok[a]) {
-                int c = f <= p ? g.cols[f - 1] : g.ycol;
-                x = g.base[(int64_t)c * g.col_stride + rowbase + r0 + a];
-                if (!__builtin_isfinite(x)) rowok[a] = 0;   // benign race: every writer stores 0
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int i = tid + j * kThreads;
+            if (i < nstage) {
+                const int f = 1 + (i >> 6), a = i & (kRows - 1);
+                const double x = pre[j];
+                if (rowok[a] && !__builtin_isfinite(x)) rowok[a] = 0;   // benign race: stores 0
+                tile[f][a] = x;
             }
-            tile[f][a] = x;
         }
         __syncthreads();
+        if (r0 + kRows < g.seg_rows) prefetch(r0 + kRows);           // in flight during MFMA
         if (wave == 0) {
             u64 m = __ballot(rowok[lane] != 0);
             if (lane == 0) flags[1] = m != 0ull;
@@ -117,7 +150,7 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(GramArgs g) {
         __syncthreads();
         if (!flags[1]) continue;                   // uniform: nothing usable in this tile
         for (int i = tid; i < p2 * kRows; i += kThreads) {
-            int f = i / kRows, a = i % kRows;
+            int f = i >> 6, a = i & (kRows - 1);
             double v = 0.0;
             if (rowok[a]) v = (f == 0) ? 1.0 : tile[f][a] - sh[f];
             tile[f][a] = v;
@@ -129,11 +162,9 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(GramArgs g) {
             const int a = ks * 4 + kk;
 #pragma unroll
             for (int q = 0; q < kMaxTiles; ++q) {
-                const int pq = wp + q * WP;
-                if (pq < npairs) {
-                    const int I = pair_I(pq, nt), J = pair_J(pq, nt);
-                    double va = tile[I * 16 + fi][a];
-                    double vb = tile[J * 16 + fi][a];
+                if (wp + q * WP < npairs) {
+                    const double va = tile[pI[q] * 16 + fi][a];
+                    const double vb = tile[pJ[q] * 16 + fi][a];
                     acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc[q], 0, 0, 0);
                 }
             }
@@ -143,21 +174,23 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(GramArgs g) {
 
     // ---- combine the WK row-groups in a fixed order, write G' (full symmetric) ----
     double* out = g.gram + (int64_t)blockIdx.x * p2 * p2;
-    double* red = &tile[0][0];               // reuse: [WK][kMaxTiles][64 lanes][4]
-    const int per = kMaxTiles * 64 * 4;
+    double* red = &tile[0][0];               // reuse: [WK][WP][kMaxTiles][64 lanes][4]
+    auto slot = [&](int k_, int q_, int r_) {
+        return (((k_ * WP + wp) * kMaxTiles + q_) * 64 + lane) * 4 + r_;
+    };
     if (WK > 1) {
         for (int q = 0; q < kMaxTiles; ++q)
-            for (int r = 0; r < 4; ++r) red[wk * per + (q * 64 + lane) * 4 + r] = acc[q][r];
+            for (int r = 0; r < 4; ++r) red[slot(wk, q, r)] = acc[q][r];
         __syncthreads();
     }
     if (wk == 0) {
         for (int q = 0; q < kMaxTiles; ++q) {
             const int pq = wp + q * WP;
             if (pq >= npairs) continue;
-            const int I = pair_I(pq, nt), J = pair_J(pq, nt);
+            const int I = pI[q], J = pJ[q];
             for (int r = 0; r < 4; ++r) {
                 double v = acc[q][r];
-                for (int k = 1; k < WK; ++k) v += red[k * per + (q * 64 + lane) * 4 + r];
+                for (int k = 1; k < WK; ++k) v += red[slot(k, q, r)];
                 const int row = I * 16 + (lane >> 4) + 4 * r;   // f64 MFMA C/D layout
                 const int col = J * 16 + (lane & 15);
                 if (row < p2 && col < p2) {
@@ -281,69 +314,58 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
     }
 }
 
-// ---- exact (Chan) combination of per-segment shifted moments over [s0, s1) -----------------
-// out: centered Gram of the union in the same "shifted" representation (shift = 0, column 0
-// carries n and the sums) so ols_solve_kernel solves the pooled problem unchanged.
+// ---- exact (Chan) combination of per-segment shifted moments ----------------------------------
+// Block b combines segments [b*per, min((b+1)*per, nseg)) in order and emits the union's moments
+// in the same "shifted" representation (G'[0][0] = n, G'[0][j] = 0, G'[i][j] = centered sums,
+// shift = mean), so a second pass (or ols_solve_kernel) consumes it unchanged.  Two passes with
+// per = 64 give the same tree for any split of the segments into 64-aligned shards (multi-GPU).
+constexpr int kPoolBlock = 64;
+
 __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, const double* shift,
-                                                        int p2, int64_t nseg, double* out_gram,
-                                                        double* out_shift) {
-    __shared__ double mu[kMaxF];       // running mean (unshifted)
-    __shared__ double dl[kMaxF];       // delta of the segment mean vs the running mean
-    __shared__ double ntot;
-    __shared__ double fac;
+                                                        int p2, int64_t nseg, int64_t per,
+                                                        double* out_gram, double* out_shift) {
+    extern __shared__ __attribute__((aligned(16))) double C[];   // [p2][p2]
+    __shared__ double mu[kMaxF];
+    __shared__ double dl[kMaxF];
+    __shared__ double ntot_s, fac_s;
     const int tid = threadIdx.x;
     const int q2 = p2 * p2;
-    constexpr int per = 40;            // this thread's centered entries (up to 40 x 256 = 10240)
-    double C[per];
-#pragma unroll
-    for (int k = 0; k < per; ++k) C[k] = 0.0;
+    const int64_t s0 = (int64_t)blockIdx.x * per;
+    const int64_t s1 = s0 + per < nseg ? s0 + per : nseg;
+    for (int e = tid; e < q2; e += kThreads) C[e] = 0.0;
     if (tid < p2) mu[tid] = 0.0;
-    if (tid == 0) ntot = 0.0;
+    if (tid == 0) ntot_s = 0.0;
     __syncthreads();
-    for (int64_t sg = 0; sg < nseg; ++sg) {
+    for (int64_t sg = s0; sg < s1; ++sg) {
         const double* G = gram + sg * q2;
         const double* S = shift + sg * p2;
         const double nb = G[0];
-        if (!(nb > 0)) continue;
-        if (tid < p2 && tid > 0) {
-            double mb = S[tid] + G[tid] / nb;        // segment mean
-            dl[tid] = mb - mu[tid];
-        }
+        if (!(nb > 0)) continue;                       // uniform
+        if (tid < p2 && tid > 0) dl[tid] = (S[tid] + G[tid] / nb) - mu[tid];
         if (tid == 0) {
-            double na = ntot;
-            fac = na * nb / (na + nb);
-            ntot = na + nb;
+            const double na = ntot_s;
+            fac_s = na * nb / (na + nb);
+            ntot_s = na + nb;
         }
         __syncthreads();
-#pragma unroll
-        for (int k = 0; k < per; ++k) {
-            int e = tid + k * kThreads;
-            if (e < q2) {
-                int r = e / p2, c = e % p2;
-                if (r > 0 && c > 0) {
-                    double cb = G[r * p2 + c] - G[r] * G[c] / nb;   // segment centered
-                    C[k] = C[k] + cb + dl[r] * dl[c] * fac;
-                }
+        const double fac = fac_s;
+        for (int e = tid; e < q2; e += kThreads) {
+            const int r = e / p2, c = e - r * p2;
+            if (r > 0 && c > 0) {
+                const double cb = G[e] - G[r] * G[c] / nb;            // segment centered
+                C[e] = C[e] + cb + dl[r] * dl[c] * fac;
             }
         }
         __syncthreads();
-        if (tid < p2 && tid > 0) mu[tid] = mu[tid] + dl[tid] * (nb / ntot);
+        if (tid < p2 && tid > 0) mu[tid] = mu[tid] + dl[tid] * (nb / ntot_s);
         __syncthreads();
     }
-    // emit as a Gram with shift = mu: G'[0][0] = n, G'[0][j] = 0 (centered), G'[i][j] = C
-#pragma unroll
-    for (int k = 0; k < per; ++k) {
-        int e = tid + k * kThreads;
-        if (e < q2) {
-            int r = e / p2, c = e % p2;
-            double v;
-            if (r == 0 && c == 0) v = ntot;
-            else if (r == 0 || c == 0) v = 0.0;
-            else v = C[k];
-            out_gram[e] = v;
-        }
+    double* og = out_gram + (int64_t)blockIdx.x * q2;
+    for (int e = tid; e < q2; e += kThreads) {
+        const int r = e / p2, c = e - r * p2;
+        og[e] = (r == 0 && c == 0) ? ntot_s : ((r == 0 || c == 0) ? 0.0 : C[e]);
     }
-    if (tid < p2) out_shift[tid] = (tid == 0) ? 0.0 : mu[tid];
+    if (tid < p2) out_shift[(int64_t)blockIdx.x * p2 + tid] = (tid == 0) ? 0.0 : mu[tid];
 }
 
 // ---- predictions: pred[t][a] = beta0 + sum_j beta_j x_j (grid rows with a set mask bit) ------
@@ -367,6 +389,29 @@ __global__ __launch_bounds__(256) void predict_kernel(const double* base, int64_
         v = s;
     }
     pred[t * lda + a] = v;
+}
+
+// ---- least-squares refinement: r = (y - ybar) - sum_j b_j (x_j - xbar_j) over a long design ----
+__global__ __launch_bounds__(256) void residual_kernel(const double* Z, int64_t n, int p, int ycol,
+                                                       const double* mean, const double* beta,
+                                                       double* r) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double s = Z[(int64_t)ycol * n + i] - mean[p + 1];
+    for (int j = 0; j < p; ++j) s = s - beta[1 + j] * (Z[(int64_t)j * n + i] - mean[1 + j]);
+    r[i] = s;
+}
+
+__global__ void vec_add_kernel(int64_t n, const double* x, double* y) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) y[i] = y[i] + x[i];
+}
+
+__global__ void intercept_kernel(int p, const double* mean, double* beta) {
+    if (threadIdx.x != 0) return;
+    double icpt = mean[p + 1];
+    for (int j = 0; j < p; ++j) icpt = icpt - mean[1 + j] * beta[1 + j];
+    beta[0] = icpt;
 }
 
 // ---- Fama-MacBeth: mean_t beta_t and t = mean / (std / sqrt(T)) over segments with rank > 0 --
@@ -426,11 +471,30 @@ extern "C" int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double*
 extern "C" int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
                                     int64_t nseg, double* out_gram, double* out_shift) {
     AFM_CTX(ctx);
-    AFM_CHECK_ARG(p >= 1 && (p + 2) * (p + 2) <= 40 * kThreads, "p too large for pooling");
-    AFM_CHECK_ARG(gram && shift && out_gram && out_shift, "null buffer");
-    hipLaunchKernelGGL(pool_kernel, dim3(1), dim3(kThreads), 0, ctx->stream, gram, shift, p + 2,
-                       nseg, out_gram, out_shift);
+    AFM_CHECK_ARG(p >= 1 && p + 2 <= kMaxF, "need 1 <= p <= 110");
+    AFM_CHECK_ARG(gram && shift && out_gram && out_shift && nseg >= 0, "bad arguments");
+    const int p2 = p + 2;
+    const size_t lds = sizeof(double) * p2 * p2;
+    AFM_HIP(hipFuncSetAttribute((const void*)pool_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int64_t nb = (nseg + kPoolBlock - 1) / kPoolBlock;
+    if (nb <= 1) {
+        hipLaunchKernelGGL(pool_kernel, dim3(1), dim3(kThreads), lds, ctx->stream, gram, shift,
+                           p2, nseg, (int64_t)kPoolBlock, out_gram, out_shift);
+        AFM_HIP(hipGetLastError());
+        return AFM_OK;
+    }
+    double* work = nullptr;
+    AFM_HIP(hipMallocAsync((void**)&work, sizeof(double) * nb * (p2 * p2 + p2), ctx->stream));
+    double* wg = work;
+    double* ws = work + nb * p2 * p2;
+    hipLaunchKernelGGL(pool_kernel, dim3((unsigned)nb), dim3(kThreads), lds, ctx->stream, gram,
+                       shift, p2, nseg, (int64_t)kPoolBlock, wg, ws);
     AFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(pool_kernel, dim3(1), dim3(kThreads), lds, ctx->stream, wg, ws, p2, nb, nb,
+                       out_gram, out_shift);
+    AFM_HIP(hipGetLastError());
+    AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;
 }
 
@@ -455,6 +519,35 @@ extern "C" int afm_fama_macbeth_f64(afm_ctx* ctx, const double* beta, const int3
     AFM_CHECK_ARG(beta && rank && mean_out && t_out && k > 0, "bad args");
     hipLaunchKernelGGL(fama_macbeth_kernel, dim3((k + 63) / 64), dim3(64), 0, ctx->stream, beta,
                        rank, nseg, k, mean_out, t_out);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_ols_residual_f64(afm_ctx* ctx, const double* Z, int64_t n, int p, int ycol,
+                                    const double* mean, const double* beta, double* r) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(Z && mean && beta && r && n >= 0 && p >= 1, "bad arguments");
+    if (n == 0) return AFM_OK;
+    hipLaunchKernelGGL(residual_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       ctx->stream, Z, n, p, ycol, mean, beta, r);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_vec_add_f64(afm_ctx* ctx, int64_t n, const double* x, double* y) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(x && y && n >= 0, "bad arguments");
+    if (n == 0) return AFM_OK;
+    hipLaunchKernelGGL(vec_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       ctx->stream, n, x, y);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_ols_intercept_f64(afm_ctx* ctx, int p, const double* mean, double* beta) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(mean && beta && p >= 1, "bad arguments");
+    hipLaunchKernelGGL(intercept_kernel, dim3(1), dim3(64), 0, ctx->stream, p, mean, beta);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

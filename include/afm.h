@@ -85,6 +85,13 @@ int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const double* shift, 
 int afm_predict_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda, int64_t t0,
                     int64_t nt, const int32_t* cols, int p, const double* beta,
                     int64_t beta_stride, const uint64_t* bits, int ycheck, double* pred);
+/* Least-squares refinement helpers for a long design Z [..][n] (column j at Z + j*n):
+ * r = (Z[ycol] - mean[p+1]) - sum_j beta[1+j] * (Z[j] - mean[1+j]) (mean = a pooled shift vector);
+ * y += x; beta[0] = mean[p+1] - sum_j mean[1+j] * beta[1+j]. */
+int afm_ols_residual_f64(afm_ctx* ctx, const double* Z, int64_t n, int p, int ycol,
+                         const double* mean, const double* beta, double* r);
+int afm_vec_add_f64(afm_ctx* ctx, int64_t n, const double* x, double* y);
+int afm_ols_intercept_f64(afm_ctx* ctx, int p, const double* mean, double* beta);
 /* Fama-MacBeth over segments with rank > 0: mean_t beta_t and mean / (std / sqrt(T)). */
 int afm_fama_macbeth_f64(afm_ctx* ctx, const double* beta, const int32_t* rank, int64_t nseg,
                          int k, double* mean_out, double* t_out);
