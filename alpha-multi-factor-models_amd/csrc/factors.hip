@@ -39,8 +39,17 @@ constexpr int kWaves = 16;
 constexpr int kLoadSteps = kChunk / kWaves;  // 4 days loaded into the ring per wave per chunk
 
 typedef unsigned long long u64;
+// explicit address spaces: the per-wave functions are not inlined, and generic (flat) pointers
+// would turn every ring read into a flat_load that waits on all outstanding global stores
+#define LDS __attribute__((address_space(3)))
+#define GLB __attribute__((address_space(1)))
 
 __device__ __forceinline__ double qnan() { return __builtin_nan(""); }
+// Workgroup barrier ordering LDS only: the ring and the NaN masks live in LDS; the output stores
+// need no ordering, so the barrier must not wait for them (__syncthreads() waits vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 __device__ __forceinline__ double pinf(double x) { return __builtin_isinf(x) ? qnan() : x; }
 // pandas zsqrt: negative -> 0, NaN stays NaN
 __device__ __forceinline__ double zsqrt(double x) { return x < 0 ? 0.0 : __builtin_sqrt(x); }
@@ -54,18 +63,18 @@ struct Smem {
 
 struct Args {
     int64_t T, lda, plane;     // plane = T * lda
-    const double* close;
-    const double* volume;
-    const uint64_t* vbits;
-    double* out;
-    uint64_t* nanfree;
-    uint64_t* finite;          // optional
+    const GLB double* close;
+    const GLB double* volume;
+    const GLB uint64_t* vbits;
+    GLB double* out;
+    GLB uint64_t* nanfree;
+    GLB uint64_t* finite;      // optional
 };
 
 // Per-lane view of one (asset, present day) step.
 struct Step {
-    const Smem* sm;
-    double* out;
+    const LDS Smem* sm;
+    GLB double* out;
     int64_t plane, cell;
     int lane, p;               // p = index of this observation in the asset's series
     bool anynan, anybad;
@@ -479,7 +488,8 @@ using W14 = Pack<Ema<6>, Ema<10>, Ema<14>, Ema<18>, Ema<22>, Ema<26>, Ema<30>, E
 using W15 = Pack<Macd<18>, Macd<24>, Macd<30>, Rsi<14>, Rsi<20>>;
 
 template <class P>
-__device__ __noinline__ void run_wave(const Args& a, Smem& sm, int wave, int lane) {
+__device__ __noinline__ void run_wave(const Args a, LDS Smem* smp, int wave, int lane) {
+    LDS Smem& sm = *smp;
     const int64_t asset = (int64_t)blockIdx.x * kLanes + lane;
     const int nch = (int)((a.T + kChunk - 1) / kChunk);
     P jobs;
@@ -524,7 +534,7 @@ __device__ __noinline__ void run_wave(const Args& a, Smem& sm, int wave, int lan
                 pv[j] = in ? a.volume[t * a.lda + asset] : 0.0;
             }
         }
-        __syncthreads();
+        lds_barrier();
 
         const int64_t t0 = (int64_t)ch * kChunk;
         const int steps = (int)min((int64_t)kChunk, a.T - t0);
@@ -533,7 +543,7 @@ __device__ __noinline__ void run_wave(const Args& a, Smem& sm, int wave, int lan
         for (int s = 0; s < steps; ++s) {
             if ((vb >> s) & 1ull) {
                 Step st;
-                st.sm = &sm;
+                st.sm = smp;
                 st.out = a.out;
                 st.plane = a.plane;
                 st.cell = (t0 + s) * a.lda + asset;
@@ -547,9 +557,9 @@ __device__ __noinline__ void run_wave(const Args& a, Smem& sm, int wave, int lan
                 ++p;
             }
         }
-        if (nb) atomicOr(&sm.nanmask[lane], nb);
-        if (fb) atomicOr(&sm.badmask[lane], fb);
-        __syncthreads();
+        if (nb) __atomic_fetch_or(&sm.nanmask[lane], nb, __ATOMIC_RELAXED);
+        if (fb) __atomic_fetch_or(&sm.badmask[lane], fb, __ATOMIC_RELAXED);
+        lds_barrier();
         if (wave == 0) {
             a.nanfree[(int64_t)ch * a.lda + asset] = vb & ~sm.nanmask[lane];
             if (a.finite) a.finite[(int64_t)ch * a.lda + asset] = vb & ~sm.badmask[lane];
@@ -559,7 +569,8 @@ __device__ __noinline__ void run_wave(const Args& a, Smem& sm, int wave, int lan
 }
 
 __global__ __launch_bounds__(kLanes * kWaves) void factor_panel_kernel(Args a) {
-    __shared__ Smem sm;
+    __shared__ Smem sm_;
+    LDS Smem* sm = (LDS Smem*)&sm_;
     const int lane = threadIdx.x & (kLanes - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     switch (wave) {
@@ -633,12 +644,12 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     a.T = T;
     a.lda = lda;
     a.plane = T * lda;
-    a.close = close;
-    a.volume = volume;
-    a.vbits = valid_bits;
-    a.out = out;
-    a.nanfree = nanfree_bits;
-    a.finite = finite_bits;
+    a.close = (const GLB double*)close;
+    a.volume = (const GLB double*)volume;
+    a.vbits = (const GLB uint64_t*)valid_bits;
+    a.out = (GLB double*)out;
+    a.nanfree = (GLB uint64_t*)nanfree_bits;
+    a.finite = (GLB uint64_t*)finite_bits;
     dim3 grid((unsigned)(lda / 64));
     hipLaunchKernelGGL(afm::factor_panel_kernel, grid, dim3(64 * 16), 0, ctx->stream, a);
     AFM_HIP(hipGetLastError());

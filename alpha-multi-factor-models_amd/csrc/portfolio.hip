@@ -527,57 +527,63 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
 }
 
 // ---- sequential value / turnover recursion (KKT:864-892) ----------------------------------
-// sparse numpy pairwise sum over a length-n vector that is zero except at sorted positions
-__device__ double pairwise_sparse(const int64_t* pos, const double* val, int m, int64_t lo,
-                                  int64_t n, int depth) {
-    // entries with lo <= pos < lo + n
-    int b = 0;
-    while (b < m && pos[b] < lo) ++b;
-    int e = b;
-    while (e < m && pos[e] < lo + n) ++e;
-    if (e == b) return 0.0;
-    if (n < 8) {
-        double res = 0.;
-        for (int q = b; q < e; ++q) res += val[q];
-        return res;
-    } else if (n <= 128) {
-        double rr[8];
-        const int64_t body = n - (n % 8);
-        for (int j = 0; j < 8; ++j) rr[j] = 0.0;
-        for (int q = b; q < e; ++q) {
-            int64_t off = pos[q] - lo;
-            if (off < body) rr[off % 8] += val[q];
+// The turnover is numpy's pairwise sum over the union-aligned vector |cur - new| (KKT:839), which
+// is zero except at the books' members.  Its summation tree is fixed by the union length and
+// the members' positions, so turnover_terms_kernel (parallel over dates) compiles it into a
+// short stack program; the sequential scan only evaluates term values (they depend on V) and
+// runs the program.  Zero slots contribute exact +0.0 (every term is |.| >= 0), so a subtree
+// without members is skipped and a node with one non-empty child passes it up unchanged.
+constexpr int kMaxTerms = 4 * kMaxK;
+constexpr int kMaxProg = 4 * kMaxTerms;
+// program tokens: >= 0 : LEAF starting at term index (token & 0xffff), count (token >> 16);
+//                 -1   : ADD (pop b, pop a, push a + b)
+struct TermBuild {
+    int pos[kMaxTerms], side[kMaxTerms], slot[kMaxTerms];
+    int prog[kMaxProg];
+    int nprog, m;
+};
+
+// symbolic numpy pairwise_sum over positions [lo, lo + n) (terms sorted by position)
+__device__ int build_pw(TermBuild& tb, int64_t lo, int64_t n, int b, int e) {
+    // returns 1 if the subtree holds a term (pushes one value), else 0
+    while (b < e && tb.pos[b] < lo) ++b;
+    int ee = b;
+    while (ee < e && tb.pos[ee] < lo + n) ++ee;
+    if (ee == b) return 0;
+    if (n <= 128) {
+        const int64_t body = n < 8 ? 0 : n - (n % 8);
+        for (int q = b; q < ee; ++q) {
+            const int64_t off = tb.pos[q] - lo;
+            tb.slot[q] = (n < 8) ? 9 : (off < body ? (int)(off % 8) : 8);   // 9 seq, 8 tail
         }
-        double res = ((rr[0] + rr[1]) + (rr[2] + rr[3])) + ((rr[4] + rr[5]) + (rr[6] + rr[7]));
-        for (int q = b; q < e; ++q)
-            if (pos[q] - lo >= body) res += val[q];
-        return res;
+        tb.prog[tb.nprog++] = b | ((ee - b) << 16);
+        return 1;
     }
     int64_t n2 = n / 2;
     n2 -= n2 % 8;
-    return pairwise_sparse(pos, val, m, lo, n2, depth + 1) +
-           pairwise_sparse(pos, val, m, lo + n2, n - n2, depth + 1);
+    const int l = build_pw(tb, lo, n2, b, ee);
+    const int r = build_pw(tb, lo + n2, n - n2, b, ee);
+    if (l && r) tb.prog[tb.nprog++] = -1;
+    return l | r;
 }
-
-// Turnover terms of date i >= 1 (structure only; the values need V): for each id in the previous
-// or current books that is predicted on both dates, its union position and its side on each date
-// (0 long, 1 short, 2 none).  Sorted by union position.  One 64-thread block per date.
-constexpr int kMaxTerms = 4 * kMaxK;
 
 __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const int32_t* k_out,
                                                             const int32_t* books,
-                                                            const int32_t* upos, int32_t* tpos,
-                                                            int32_t* tside, int32_t* tcount) {
+                                                            const int32_t* upos,
+                                                            const int64_t* usize, int32_t* tside,
+                                                            int32_t* tslot, int32_t* tprog,
+                                                            int32_t* tcount) {
+    __shared__ TermBuild tb;
     __shared__ int pos_s[kMaxTerms], side_s[kMaxTerms];
     __shared__ int cnt;
     const int64_t i = blockIdx.x;
     const int tid = threadIdx.x;
     if (tid == 0) cnt = 0;
     __syncthreads();
-    if (i > 0 && k_out[i - 1] > 0) {          // current_positions.dropna().empty -> 0 (KKT:836)
+    const bool active = i > 0 && k_out[i - 1] > 0;   // current_positions.dropna().empty -> 0
+    if (active) {
         const int k = k_out[i], kp = k_out[i - 1];
-        // previous members predicted today
-        for (int e = tid; e < 2 * kp; e += 64) {
+        for (int e = tid; e < 2 * kp; e += 64) {     // previous members predicted today
             const int side = e / kp, q = e % kp;
             const int a = books[((i - 1) * 2 + side) * kMaxK + q];
             const int pz = upos[(((i - 1) * 2 + side) * 2 + 1) * kMaxK + q];
@@ -590,8 +596,7 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
             pos_s[slot] = pz;
             side_s[slot] = side * 3 + ns;
         }
-        // current members predicted yesterday and not in yesterday's books
-        for (int e = tid; e < 2 * k; e += 64) {
+        for (int e = tid; e < 2 * k; e += 64) {      // today's members predicted yesterday only
             const int side = e / k, q = e % k;
             const int a = books[(i * 2 + side) * kMaxK + q];
             const int pz = upos[((i * 2 + side) * 2 + 0) * kMaxK + q];
@@ -608,60 +613,120 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
     }
     __syncthreads();
     const int m = cnt;
-    for (int e = tid; e < m; e += 64) {       // rank by count (positions are distinct)
+    for (int e = tid; e < m; e += 64) {              // sort by union position (distinct)
         int r = 0;
         for (int f = 0; f < m; ++f) r += pos_s[f] < pos_s[e];
-        tpos[i * kMaxTerms + r] = pos_s[e];
-        tside[i * kMaxTerms + r] = side_s[e];
+        tb.pos[r] = pos_s[e];
+        tb.side[r] = side_s[e];
     }
-    if (tid == 0) tcount[i] = i > 0 && k_out[i - 1] > 0 ? m : -1;
+    __syncthreads();
+    if (tid == 0) {
+        tb.nprog = 0;
+        if (m > 0) build_pw(tb, 0, usize[i * 2 + 0], 0, m);
+        tcount[i * 2 + 0] = active ? m : -1;
+        tcount[i * 2 + 1] = tb.nprog;
+    }
+    __syncthreads();
+    for (int e = tid; e < m; e += 64) {
+        tside[i * kMaxTerms + e] = tb.side[e];
+        tslot[i * kMaxTerms + e] = tb.slot[e];
+    }
+    for (int e = tid; e < tb.nprog; e += 64) tprog[i * kMaxProg + e] = tb.prog[e];
 }
 
-// The value recursion (KKT:864-892).  Per date the term values |c - n| are formed in parallel
-// (c, n = +-(V/2)/den exactly as the reference computes them), the turnover is numpy's pairwise
-// sum over the aligned union vector evaluated at the terms' positions, then V advances.
-__global__ __launch_bounds__(64) void pnl_scan_kernel(int64_t nd, const double* sums,
-                                                      const int32_t* tpos, const int32_t* tside,
-                                                      const int32_t* tcount, const int64_t* usize,
-                                                      double v0, double rate, double* value,
+struct ScanBuf {
+    int side[kMaxTerms], slot[kMaxTerms], prog[kMaxProg];
+    double sums[4], sums_prev[4];
+    int m, nprog;
+};
+
+__global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double* sums,
+                                                      const int32_t* tside, const int32_t* tslot,
+                                                      const int32_t* tprog,
+                                                      const int32_t* tcount, double v0,
+                                                      double rate, double* value,
                                                       double* turnover, double* long_ret,
                                                       double* short_ret) {
-    __shared__ int64_t pos_s[kMaxTerms];
-    __shared__ double val_s[kMaxTerms];
-    __shared__ double Vs;
+    __shared__ ScanBuf buf[2];
+    __shared__ double val[kMaxTerms];
+    __shared__ double Vs, Vprev;
     const int tid = threadIdx.x;
-    if (tid == 0) { Vs = v0; value[0] = v0; }
+    // wave 1 (threads 64..127) stages date i+1 while lane 0 of wave 0 runs date i's program
+    auto load = [&](int64_t i, ScanBuf& B) {
+        const int lt = tid - 64;
+        const int m = tcount[i * 2 + 0], np = tcount[i * 2 + 1];
+        for (int e = lt; e < m; e += 64) {
+            B.side[e] = tside[i * kMaxTerms + e];
+            B.slot[e] = tslot[i * kMaxTerms + e];
+        }
+        for (int e = lt; e < np; e += 64) B.prog[e] = tprog[i * kMaxProg + e];
+        if (lt < 4) {
+            B.sums[lt] = sums[i * 4 + lt];
+            B.sums_prev[lt] = i > 0 ? sums[(i - 1) * 4 + lt] : 0.0;
+        }
+        if (lt == 0) { B.m = m; B.nprog = np; }
+    };
+    if (tid == 0) { Vs = v0; Vprev = v0; value[0] = v0; }
+    if (tid >= 64) load(0, buf[0]);
     __syncthreads();
     for (int64_t i = 0; i < nd; ++i) {
-        const double V = Vs;
-        const double* sm = sums + i * 4;
-        const int m = tcount[i];
-        if (m > 0) {
-            const double* sp = sums + (i - 1) * 4;
-            const double Vp = value[i - 1];
+        ScanBuf& B = buf[i & 1];
+        const double V = Vs, Vp = Vprev;
+        const int m = B.m;
+        if (m > 0) {                                  // term values |c - n| (KKT:881-882, 839)
             const double sizep = Vp / 2, size = V / 2;
-            for (int e = tid; e < m; e += 64) {
-                const int sd = tside[i * kMaxTerms + e];
+            for (int e = tid; e < m; e += 128) {
+                const int sd = B.side[e];
                 const int ps = sd / 3, ns = sd % 3;
-                const double c = ps == 0 ? sizep / sp[2] : (ps == 1 ? -sizep / sp[3] : 0.0);
-                const double n = ns == 0 ? size / sm[2] : (ns == 1 ? -size / sm[3] : 0.0);
-                const double d = c - n;
-                val_s[e] = d < 0 ? -d : d;
-                pos_s[e] = tpos[i * kMaxTerms + e];
+                const double c = ps == 0 ? sizep / B.sums_prev[2]
+                                         : (ps == 1 ? -sizep / B.sums_prev[3] : 0.0);
+                const double nv = ns == 0 ? size / B.sums[2] : (ns == 1 ? -size / B.sums[3] : 0.0);
+                const double d = c - nv;
+                val[e] = d < 0 ? -d : d;
             }
         }
         __syncthreads();
         if (tid == 0) {
-            double daily = (sm[0] - sm[1]) / 2;
-            long_ret[i] = sm[0];
-            short_ret[i] = sm[1];
             double to = 0.0;
-            if (m > 0) to = pairwise_sparse(pos_s, val_s, m, 0, usize[i * 2 + 0], 0) / 2;
+            if (m > 0) {
+                double stk[16];
+                int sp = 0;
+                for (int q = 0; q < B.nprog; ++q) {
+                    const int tk = B.prog[q];
+                    if (tk < 0) {
+                        const double bb = stk[--sp];
+                        const double aa = stk[--sp];
+                        stk[sp++] = aa + bb;
+                        continue;
+                    }
+                    const int t0 = tk & 0xffff, cnt = tk >> 16;
+                    double res;
+                    if (B.slot[t0] == 9) {            // leaf shorter than 8: sequential from 0
+                        res = 0.;
+                        for (int e = t0; e < t0 + cnt; ++e) res += val[e];
+                    } else {                          // 8 accumulators, then the tail
+                        double r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                        for (int e = t0; e < t0 + cnt; ++e)
+                            if (B.slot[e] < 8) r[B.slot[e]] += val[e];
+                        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                        for (int e = t0; e < t0 + cnt; ++e)
+                            if (B.slot[e] == 8) res += val[e];
+                    }
+                    stk[sp++] = res;
+                }
+                to = stk[0] / 2;
+            }
+            double daily = (B.sums[0] - B.sums[1]) / 2;
+            long_ret[i] = B.sums[0];
+            short_ret[i] = B.sums[1];
             turnover[i] = to;
             daily -= (to * rate) / V;
             const double Vn = V * (1 + daily);
             value[i + 1] = Vn;
+            Vprev = V;
             Vs = Vn;
+        } else if (tid >= 64 && i + 1 < nd) {
+            load(i + 1, buf[(i + 1) & 1]);
         }
         __syncthreads();
     }
@@ -707,16 +772,17 @@ extern "C" int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out,
                       short_ret, "null buffer");
     if (nd <= 0) return AFM_OK;
     int32_t* work = nullptr;
-    const size_t words = (size_t)nd * (2 * kMaxTerms + 1);
+    const size_t words = (size_t)nd * (2 * kMaxTerms + kMaxProg + 2);
     AFM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * words, ctx->stream));
-    int32_t* tpos = work;
-    int32_t* tside = work + nd * kMaxTerms;
-    int32_t* tcount = work + 2 * nd * kMaxTerms;
+    int32_t* tside = work;
+    int32_t* tslot = work + nd * kMaxTerms;
+    int32_t* tprog = work + 2 * nd * kMaxTerms;
+    int32_t* tcount = tprog + nd * kMaxProg;
     hipLaunchKernelGGL(turnover_terms_kernel, dim3((unsigned)nd), dim3(64), 0, ctx->stream, nd,
-                       k_out, books, upos, tpos, tside, tcount);
+                       k_out, books, upos, usize, tside, tslot, tprog, tcount);
     AFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(pnl_scan_kernel, dim3(1), dim3(64), 0, ctx->stream, nd, sums, tpos, tside,
-                       tcount, usize, v0, rate, value, turnover, long_ret, short_ret);
+    hipLaunchKernelGGL(pnl_scan_kernel, dim3(1), dim3(128), 0, ctx->stream, nd, sums, tside, tslot,
+                       tprog, tcount, v0, rate, value, turnover, long_ret, short_ret);
     AFM_HIP(hipGetLastError());
     AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;
