@@ -649,6 +649,7 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                                                       double* short_ret) {
     __shared__ ScanBuf buf[2];
     __shared__ double val[kMaxTerms];
+    __shared__ double stk[kMaxTerms + 1];
     __shared__ double Vs, Vprev;
     const int tid = threadIdx.x;
     // wave 1 (threads 64..127) stages date i+1 while lane 0 of wave 0 runs date i's program
@@ -668,7 +669,7 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
     };
     if (tid == 0) { Vs = v0; Vprev = v0; value[0] = v0; }
     if (tid >= 64) load(0, buf[0]);
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     for (int64_t i = 0; i < nd; ++i) {
         ScanBuf& B = buf[i & 1];
         const double V = Vs, Vp = Vprev;
@@ -685,11 +686,10 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                 val[e] = d < 0 ? -d : d;
             }
         }
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (tid == 0) {
             double to = 0.0;
             if (m > 0) {
-                double stk[16];
                 int sp = 0;
                 for (int q = 0; q < B.nprog; ++q) {
                     const int tk = B.prog[q];
@@ -728,7 +728,7 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
         } else if (tid >= 64 && i + 1 < nd) {
             load(i + 1, buf[(i + 1) & 1]);
         }
-        __syncthreads();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 }
 
