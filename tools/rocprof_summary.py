@@ -38,7 +38,7 @@ def main():
     lines = [f"source: {os.path.basename(src)}", "",
              "| kernel | calls | avg ms | total ms | % |", "|---|---:|---:|---:|---:|"]
     for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
-        short = name.split("(")[0]
+        short = name.replace("(anonymous namespace)::", "").split("(")[0]
         if short.startswith("_ZN3afm"):
             short = short.replace("_ZN3afm12_GLOBAL__N_1", "afm::")
         lines.append(f"| {short[:80]} | {len(v)} | {sum(v) / len(v) / 1e6:.3f} | "
