@@ -528,56 +528,84 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
 
 // ---- sequential value / turnover recursion (KKT:864-892) ----------------------------------
 // The turnover is numpy's pairwise sum over the union-aligned vector |cur - new| (KKT:839), which
-// is zero except at the books' members.  Its summation tree is fixed by the union length and
-// the members' positions, so turnover_terms_kernel (parallel over dates) compiles it into a
-// short stack program; the sequential scan only evaluates term values (they depend on V) and
-// runs the program.  Zero slots contribute exact +0.0 (every term is |.| >= 0), so a subtree
-// without members is skipped and a node with one non-empty child passes it up unchanged.
-constexpr int kMaxTerms = 4 * kMaxK;
-constexpr int kMaxProg = 4 * kMaxTerms;
-// program tokens: >= 0 : LEAF starting at term index (token & 0xffff), count (token >> 16);
-//                 -1   : ADD (pop b, pop a, push a + b)
-struct TermBuild {
-    int pos[kMaxTerms], side[kMaxTerms], slot[kMaxTerms];
-    int prog[kMaxProg];
-    int nprog, m;
+// is zero except at the books' members.  Zero slots contribute exact +0.0 (every term is
+// |.| >= 0), so the summation tree restricted to the members is a DAG of binary adds over the
+// member terms whose shape depends only on the union length and the members' positions -- not
+// on the portfolio value.  turnover_terms_kernel (parallel over dates) compiles each date's DAG
+// into a record of LEVELS (every add of level l depends only on lower levels); the sequential
+// scan then evaluates one date as: term values (lane-parallel), one lane-parallel step per DAG
+// level, the value update -- all out of LDS, with records staged a chunk of dates ahead.
+constexpr int kMaxTerms = 4 * kMaxK;        // terms of one date (<= 2 books x 2 dates x k)
+// DAG depth <= 16 (one accumulator of a 128-wide leaf) + 3 + 7 (tail) + log2(65536 / 128) = 35
+constexpr int kMaxLevels = 64;
+constexpr int kRec = 4 + 2 * kMaxTerms + kMaxLevels;   // record words (fixed global stride)
+// record: [0] m (terms; -1: no turnover that date) [1] nint (adds) [2] L (levels) [3] unused,
+//         [4, 4+m) term codes (3 * prev side + new side; side 2 = absent),
+//         [4+m, 4+m+nint) adds in level order: left | right << 16 (node ids: terms 0..m-1,
+//         add q -> m + q), then L cumulative add counts per level.
+struct Dag {
+    int m, nint;
+    int l[kMaxTerms], r[kMaxTerms];
+    int lev[2 * kMaxTerms];
 };
 
-// symbolic numpy pairwise_sum over positions [lo, lo + n) (terms sorted by position)
-__device__ int build_pw(TermBuild& tb, int64_t lo, int64_t n, int b, int e) {
-    // returns 1 if the subtree holds a term (pushes one value), else 0
-    while (b < e && tb.pos[b] < lo) ++b;
+__device__ int dag_add(Dag& d, int a, int b) {
+    if (a < 0) return b;
+    if (b < 0) return a;
+    const int id = d.m + d.nint;
+    d.l[d.nint] = a;
+    d.r[d.nint] = b;
+    d.lev[id] = (d.lev[a] > d.lev[b] ? d.lev[a] : d.lev[b]) + 1;
+    d.nint++;
+    return id;
+}
+
+// symbolic numpy pairwise_sum over positions [lo, lo + n) restricted to the terms [b, e) (sorted
+// by position): returns the node holding the subtree's sum, -1 if the subtree has no term
+__device__ int build_dag(Dag& d, const int* pos, int64_t lo, int64_t n, int b, int e) {
+    while (b < e && pos[b] < lo) ++b;
     int ee = b;
-    while (ee < e && tb.pos[ee] < lo + n) ++ee;
-    if (ee == b) return 0;
+    while (ee < e && pos[ee] < lo + n) ++ee;
+    if (ee == b) return -1;
     if (n <= 128) {
-        const int64_t body = n < 8 ? 0 : n - (n % 8);
-        for (int q = b; q < ee; ++q) {
-            const int64_t off = tb.pos[q] - lo;
-            tb.slot[q] = (n < 8) ? 9 : (off < body ? (int)(off % 8) : 8);   // 9 seq, 8 tail
+        if (n < 8) {                                       // res = 0.; res += a[i]
+            int acc = -1;
+            for (int q = b; q < ee; ++q) acc = dag_add(d, acc, q);
+            return acc;
         }
-        tb.prog[tb.nprog++] = b | ((ee - b) << 16);
-        return 1;
+        const int64_t body = n - (n % 8);                  // 8 strided accumulators, then tail
+        int r[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+        for (int q = b; q < ee; ++q) {
+            const int64_t off = pos[q] - lo;
+            if (off < body) r[off % 8] = dag_add(d, r[off % 8], q);
+        }
+        const int r01 = dag_add(d, r[0], r[1]), r23 = dag_add(d, r[2], r[3]);
+        const int r45 = dag_add(d, r[4], r[5]), r67 = dag_add(d, r[6], r[7]);
+        const int lo4 = dag_add(d, r01, r23), hi4 = dag_add(d, r45, r67);
+        int res = dag_add(d, lo4, hi4);
+        for (int q = b; q < ee; ++q)
+            if (pos[q] - lo >= body) res = dag_add(d, res, q);
+        return res;
     }
     int64_t n2 = n / 2;
     n2 -= n2 % 8;
-    const int l = build_pw(tb, lo, n2, b, ee);
-    const int r = build_pw(tb, lo + n2, n - n2, b, ee);
-    if (l && r) tb.prog[tb.nprog++] = -1;
-    return l | r;
+    const int L = build_dag(d, pos, lo, n2, b, ee);
+    const int R = build_dag(d, pos, lo + n2, n - n2, b, ee);
+    return dag_add(d, L, R);
 }
 
 __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const int32_t* k_out,
                                                             const int32_t* books,
                                                             const int32_t* upos,
-                                                            const int64_t* usize, int32_t* tside,
-                                                            int32_t* tslot, int32_t* tprog,
-                                                            int32_t* tcount) {
-    __shared__ TermBuild tb;
-    __shared__ int pos_s[kMaxTerms], side_s[kMaxTerms];
-    __shared__ int cnt;
+                                                            const int64_t* usize, int32_t* rec,
+                                                            int32_t* rlen) {
+    __shared__ Dag dag;
+    __shared__ int pos_s[kMaxTerms], code_s[kMaxTerms], pos_o[kMaxTerms], code_o[kMaxTerms];
+    __shared__ int newid[kMaxTerms], lcount[kMaxLevels + 1];
+    __shared__ int cnt, nlev;
     const int64_t i = blockIdx.x;
     const int tid = threadIdx.x;
+    int32_t* R = rec + i * kRec;
     if (tid == 0) cnt = 0;
     __syncthreads();
     const bool active = i > 0 && k_out[i - 1] > 0;   // current_positions.dropna().empty -> 0
@@ -594,7 +622,7 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
                     if (books[(i * 2 + s2) * kMaxK + q2] == a) ns = s2;
             const int slot = atomicAdd(&cnt, 1);
             pos_s[slot] = pz;
-            side_s[slot] = side * 3 + ns;
+            code_s[slot] = side * 3 + ns;
         }
         for (int e = tid; e < 2 * k; e += 64) {      // today's members predicted yesterday only
             const int side = e / k, q = e % k;
@@ -608,7 +636,7 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
             if (inprev) continue;
             const int slot = atomicAdd(&cnt, 1);
             pos_s[slot] = pz;
-            side_s[slot] = 2 * 3 + side;
+            code_s[slot] = 2 * 3 + side;
         }
     }
     __syncthreads();
@@ -616,119 +644,153 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
     for (int e = tid; e < m; e += 64) {              // sort by union position (distinct)
         int r = 0;
         for (int f = 0; f < m; ++f) r += pos_s[f] < pos_s[e];
-        tb.pos[r] = pos_s[e];
-        tb.side[r] = side_s[e];
+        pos_o[r] = pos_s[e];
+        code_o[r] = code_s[e];
     }
     __syncthreads();
     if (tid == 0) {
-        tb.nprog = 0;
-        if (m > 0) build_pw(tb, 0, usize[i * 2 + 0], 0, m);
-        tcount[i * 2 + 0] = active ? m : -1;
-        tcount[i * 2 + 1] = tb.nprog;
+        dag.m = m;
+        dag.nint = 0;
+        for (int q = 0; q < m; ++q) dag.lev[q] = 0;
+        int L = 0;
+        if (m > 0) {
+            const int root = build_dag(dag, pos_o, 0, usize[i * 2 + 0], 0, m);
+            L = dag.lev[root];
+        }
+        nlev = L;
+        for (int l = 0; l <= L; ++l) lcount[l] = 0;
+        for (int q = 0; q < dag.nint; ++q) lcount[dag.lev[m + q]]++;
+        int acc = 0;                                  // lcount[l] -> first slot of level l
+        for (int l = 1; l <= L; ++l) { const int c = lcount[l]; lcount[l] = acc; acc += c; }
+        for (int q = 0; q < dag.nint; ++q) newid[q] = lcount[dag.lev[m + q]]++;
+        R[0] = active ? m : -1;
+        R[1] = dag.nint;
+        R[2] = L;
+        R[3] = 0;
+        rlen[i] = 4 + (active ? m : 0) + dag.nint + L;
     }
     __syncthreads();
-    for (int e = tid; e < m; e += 64) {
-        tside[i * kMaxTerms + e] = tb.side[e];
-        tslot[i * kMaxTerms + e] = tb.slot[e];
+    const int nint = dag.nint, L = nlev;
+    for (int e = tid; e < m; e += 64) R[4 + e] = code_o[e];
+    for (int q = tid; q < nint; q += 64) {
+        const int a = dag.l[q], b = dag.r[q];
+        const int na = a < m ? a : m + newid[a - m];
+        const int nb = b < m ? b : m + newid[b - m];
+        R[4 + m + newid[q]] = na | (nb << 16);
     }
-    for (int e = tid; e < tb.nprog; e += 64) tprog[i * kMaxProg + e] = tb.prog[e];
+    for (int l = tid; l < L; l += 64) R[4 + m + nint + l] = lcount[l + 1];   // cumulative ends
 }
 
-struct ScanBuf {
-    int side[kMaxTerms], slot[kMaxTerms], prog[kMaxProg];
-    double sums[4], sums_prev[4];
-    int m, nprog;
-};
+constexpr int kChunkDates = 64;
+constexpr int kBufWords = 12288;
 
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// One workgroup of 2 waves.  Wave 1 stages chunk c+1 (records + sums) into LDS while wave 0
+// runs chunk c; one barrier per chunk.  Wave 0 keeps V / V_prev replicated in every lane.
 __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double* sums,
-                                                      const int32_t* tside, const int32_t* tslot,
-                                                      const int32_t* tprog,
-                                                      const int32_t* tcount, double v0,
-                                                      double rate, double* value,
+                                                      const int32_t* rec, const int32_t* rlen,
+                                                      double v0, double rate, double* value,
                                                       double* turnover, double* long_ret,
                                                       double* short_ret) {
-    __shared__ ScanBuf buf[2];
-    __shared__ double val[kMaxTerms];
-    __shared__ double stk[kMaxTerms + 1];
-    __shared__ double Vs, Vprev;
-    const int tid = threadIdx.x;
-    // wave 1 (threads 64..127) stages date i+1 while lane 0 of wave 0 runs date i's program
-    auto load = [&](int64_t i, ScanBuf& B) {
-        const int lt = tid - 64;
-        const int m = tcount[i * 2 + 0], np = tcount[i * 2 + 1];
-        for (int e = lt; e < m; e += 64) {
-            B.side[e] = tside[i * kMaxTerms + e];
-            B.slot[e] = tslot[i * kMaxTerms + e];
+    __shared__ int buf[2][kBufWords];
+    __shared__ int offs[2][kChunkDates];
+    __shared__ double sm[2][kChunkDates + 1][4];
+    __shared__ int64_t cstart[2];
+    __shared__ int ccount[2];
+    __shared__ double node[2 * kMaxTerms];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+    // loader (wave 1): stage the dates [i0, i0 + c) into buffer b; returns i0 + c
+    auto stage = [&](int64_t i0, int b) -> int64_t {
+        int len = 0;
+        if (i0 + lane < nd) len = rlen[i0 + lane];
+        int incl = len;                                            // wave inclusive scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const int x = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += x;
         }
-        for (int e = lt; e < np; e += 64) B.prog[e] = tprog[i * kMaxProg + e];
-        if (lt < 4) {
-            B.sums[lt] = sums[i * 4 + lt];
-            B.sums_prev[lt] = i > 0 ? sums[(i - 1) * 4 + lt] : 0.0;
+        const bool fits = (i0 + lane < nd) && incl <= kBufWords;
+        const u64 fm = __ballot(fits);
+        const int c = fm == ~0ull ? 64 : __builtin_ctzll(~fm);   // prefix of dates that fits
+        if (lane < c) offs[b][lane] = incl - len;
+        for (int j = 0; j < c; ++j) {
+            const int o = __shfl(incl - len, j, 64), l = __shfl(len, j, 64);
+            const int32_t* src = rec + (i0 + j) * kRec;
+            for (int e = lane; e < l; e += 64) buf[b][o + e] = src[e];
         }
-        if (lt == 0) { B.m = m; B.nprog = np; }
+        for (int e = lane; e < (c + 1) * 4; e += 64) {
+            const int64_t ii = i0 - 1 + e / 4;
+            sm[b][e / 4][e % 4] = ii >= 0 ? sums[ii * 4 + e % 4] : 0.0;
+        }
+        if (lane == 0) { cstart[b] = i0; ccount[b] = c; }
+        return i0 + c;
     };
-    if (tid == 0) { Vs = v0; Vprev = v0; value[0] = v0; }
-    if (tid >= 64) load(0, buf[0]);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    for (int64_t i = 0; i < nd; ++i) {
-        ScanBuf& B = buf[i & 1];
-        const double V = Vs, Vp = Vprev;
-        const int m = B.m;
-        if (m > 0) {                                  // term values |c - n| (KKT:881-882, 839)
-            const double sizep = Vp / 2, size = V / 2;
-            for (int e = tid; e < m; e += 128) {
-                const int sd = B.side[e];
-                const int ps = sd / 3, ns = sd % 3;
-                const double c = ps == 0 ? sizep / B.sums_prev[2]
-                                         : (ps == 1 ? -sizep / B.sums_prev[3] : 0.0);
-                const double nv = ns == 0 ? size / B.sums[2] : (ns == 1 ? -size / B.sums[3] : 0.0);
-                const double d = c - nv;
-                val[e] = d < 0 ? -d : d;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (tid == 0) {
-            double to = 0.0;
-            if (m > 0) {
-                int sp = 0;
-                for (int q = 0; q < B.nprog; ++q) {
-                    const int tk = B.prog[q];
-                    if (tk < 0) {
-                        const double bb = stk[--sp];
-                        const double aa = stk[--sp];
-                        stk[sp++] = aa + bb;
-                        continue;
+
+    int64_t next = 0;
+    if (wave == 1) next = stage(0, 0);
+    __syncthreads();
+    double V = v0, Vp = v0;
+    if (wave == 0 && lane == 0) value[0] = v0;
+    for (int ch = 0;; ++ch) {
+        const int b = ch & 1;
+        const int c = ccount[b];
+        if (c == 0) break;                                        // uniform (read after barrier)
+        if (wave == 1) {
+            if (next < nd) next = stage(next, b ^ 1);
+            else if (lane == 0) ccount[b ^ 1] = 0;
+        } else {
+            const int64_t i0 = cstart[b];
+            for (int j = 0; j < c; ++j) {
+                const int* R = &buf[b][offs[b][j]];
+                const double* S = sm[b][j + 1];
+                const double* Sp = sm[b][j];
+                const int m = R[0];
+                double to = 0.0;
+                if (m > 0) {
+                    const int nint = R[1], L = R[2];
+                    const double sizep = Vp / 2, size = V / 2;
+                    for (int e = lane; e < m; e += 64) {              // term values |c - n|
+                        const int sd = R[4 + e];
+                        const int ps = sd / 3, ns = sd % 3;
+                        const double cv = ps == 0 ? sizep / Sp[2] : (ps == 1 ? -sizep / Sp[3] : 0.0);
+                        const double nv = ns == 0 ? size / S[2] : (ns == 1 ? -size / S[3] : 0.0);
+                        const double d = cv - nv;
+                        node[e] = d < 0 ? -d : d;
                     }
-                    const int t0 = tk & 0xffff, cnt = tk >> 16;
-                    double res;
-                    if (B.slot[t0] == 9) {            // leaf shorter than 8: sequential from 0
-                        res = 0.;
-                        for (int e = t0; e < t0 + cnt; ++e) res += val[e];
-                    } else {                          // 8 accumulators, then the tail
-                        double r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                        for (int e = t0; e < t0 + cnt; ++e)
-                            if (B.slot[e] < 8) r[B.slot[e]] += val[e];
-                        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-                        for (int e = t0; e < t0 + cnt; ++e)
-                            if (B.slot[e] == 8) res += val[e];
+                    lds_sync();
+                    const int* adds = R + 4 + m;
+                    const int* lend = adds + nint;
+                    int st = 0;
+                    for (int l = 0; l < L; ++l) {                     // one DAG level per step
+                        const int en = lend[l];
+                        for (int e = st + lane; e < en; e += 64) {
+                            const int w = adds[e];
+                            node[m + e] = node[w & 0xffff] + node[w >> 16];
+                        }
+                        st = en;
+                        lds_sync();
                     }
-                    stk[sp++] = res;
+                    to = node[nint > 0 ? m + nint - 1 : 0] / 2;
                 }
-                to = stk[0] / 2;
+                double daily = (S[0] - S[1]) / 2;
+                daily -= (to * rate) / V;
+                const double Vn = V * (1 + daily);
+                if (lane == 0) {
+                    const int64_t i = i0 + j;
+                    long_ret[i] = S[0];
+                    short_ret[i] = S[1];
+                    turnover[i] = to;
+                    value[i + 1] = Vn;
+                }
+                Vp = V;
+                V = Vn;
+                lds_sync();                                           // node[] reused next date
             }
-            double daily = (B.sums[0] - B.sums[1]) / 2;
-            long_ret[i] = B.sums[0];
-            short_ret[i] = B.sums[1];
-            turnover[i] = to;
-            daily -= (to * rate) / V;
-            const double Vn = V * (1 + daily);
-            value[i + 1] = Vn;
-            Vprev = V;
-            Vs = Vn;
-        } else if (tid >= 64 && i + 1 < nd) {
-            load(i + 1, buf[(i + 1) & 1]);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __syncthreads();
     }
 }
 
@@ -772,17 +834,14 @@ extern "C" int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out,
                       short_ret, "null buffer");
     if (nd <= 0) return AFM_OK;
     int32_t* work = nullptr;
-    const size_t words = (size_t)nd * (2 * kMaxTerms + kMaxProg + 2);
-    AFM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * words, ctx->stream));
-    int32_t* tside = work;
-    int32_t* tslot = work + nd * kMaxTerms;
-    int32_t* tprog = work + 2 * nd * kMaxTerms;
-    int32_t* tcount = tprog + nd * kMaxProg;
+    AFM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * (size_t)nd * (kRec + 1), ctx->stream));
+    int32_t* rec = work;
+    int32_t* rlen = work + nd * kRec;
     hipLaunchKernelGGL(turnover_terms_kernel, dim3((unsigned)nd), dim3(64), 0, ctx->stream, nd,
-                       k_out, books, upos, usize, tside, tslot, tprog, tcount);
+                       k_out, books, upos, usize, rec, rlen);
     AFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(pnl_scan_kernel, dim3(1), dim3(128), 0, ctx->stream, nd, sums, tside, tslot,
-                       tprog, tcount, v0, rate, value, turnover, long_ret, short_ret);
+    hipLaunchKernelGGL(pnl_scan_kernel, dim3(1), dim3(128), 0, ctx->stream, nd, sums, rec, rlen, v0,
+                       rate, value, turnover, long_ret, short_ret);
     AFM_HIP(hipGetLastError());
     AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;

@@ -415,22 +415,41 @@ __global__ void intercept_kernel(int p, const double* mean, double* beta) {
 }
 
 // ---- Fama-MacBeth: mean_t beta_t and t = mean / (std / sqrt(T)) over segments with rank > 0 --
-__global__ void fama_macbeth_kernel(const double* beta, const int32_t* rank, int64_t nseg, int k,
-                                    double* mean_out, double* t_out) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= k) return;
-    double n = 0, m = 0, m2 = 0;
-    for (int64_t s = 0; s < nseg; ++s) {
-        if (rank[s] <= 0) continue;
-        double x = beta[s * k + j];
-        n += 1;
-        double d = x - m;
-        m += d / n;
-        m2 += d * (x - m);
+// One workgroup per coefficient: two passes (sum, then squared deviations from the mean), each a
+// strided per-thread sum followed by a fixed-order tree over the 256 threads (deterministic).
+__device__ double block_sum256(double v, double* red) {
+    const int tid = threadIdx.x;
+    red[tid] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) red[tid] = red[tid] + red[tid + o];
+        __syncthreads();
     }
-    double sd = n > 1 ? __builtin_sqrt(m2 / (n - 1)) : __builtin_nan("");
-    mean_out[j] = n > 0 ? m : __builtin_nan("");
-    t_out[j] = m / (sd / __builtin_sqrt(n));
+    const double r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(256) void fama_macbeth_kernel(const double* beta, const int32_t* rank,
+                                                           int64_t nseg, int k, double* mean_out,
+                                                           double* t_out) {
+    __shared__ double red[256];
+    const int j = blockIdx.x, tid = threadIdx.x;
+    double n = 0, s = 0;
+    for (int64_t q = tid; q < nseg; q += 256)
+        if (rank[q] > 0) { n += 1; s += beta[q * k + j]; }
+    n = block_sum256(n, red);
+    s = block_sum256(s, red);
+    const double m = s / n;
+    double ss = 0;
+    for (int64_t q = tid; q < nseg; q += 256)
+        if (rank[q] > 0) { const double d = beta[q * k + j] - m; ss += d * d; }
+    ss = block_sum256(ss, red);
+    if (tid == 0) {
+        const double sd = n > 1 ? __builtin_sqrt(ss / (n - 1)) : __builtin_nan("");
+        mean_out[j] = n > 0 ? m : __builtin_nan("");
+        t_out[j] = m / (sd / __builtin_sqrt(n));
+    }
 }
 
 }  // namespace
@@ -517,7 +536,7 @@ extern "C" int afm_fama_macbeth_f64(afm_ctx* ctx, const double* beta, const int3
                                     int64_t nseg, int k, double* mean_out, double* t_out) {
     AFM_CTX(ctx);
     AFM_CHECK_ARG(beta && rank && mean_out && t_out && k > 0, "bad args");
-    hipLaunchKernelGGL(fama_macbeth_kernel, dim3((k + 63) / 64), dim3(64), 0, ctx->stream, beta,
+    hipLaunchKernelGGL(fama_macbeth_kernel, dim3(k), dim3(256), 0, ctx->stream, beta,
                        rank, nseg, k, mean_out, t_out);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
