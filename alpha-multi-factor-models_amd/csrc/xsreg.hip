@@ -6,14 +6,17 @@
 // (rows = the assets present that day, read straight from the factor planes), or one block of
 // rows of a long design matrix (the LinearRegression drop-in, KKT:582-590).
 //
-// Gram kernel (one workgroup = 4 waves per segment):
+// Gram kernel (one workgroup = 4 waves per segment, two workgroups per CU):
 //   Z = [1, x_1 .. x_p, y] over the segment's usable rows (mask bit set and every value finite),
 //   shifted by the first usable row s (Z - s keeps the moments well conditioned; column 0 is
 //   not shifted), G' = sum_rows (z - s)(z - s)^T.  Rows are staged 64 at a time through an LDS
-//   tile [feature][row] (row stride 66 doubles -> conflict-free fragment reads) and reduced with
-//   v_mfma_f64_16x16x4_f64 over the upper-triangle 16x16 tile pairs; waves split tile pairs
-//   (wide designs) and/or rows (narrow designs), partial sums are combined in a fixed order, so
-//   results are deterministic.
+//   tile [feature][row] (row stride 66 doubles -> conflict-free fragment reads); the regressor
+//   block X'X goes to v_mfma_f64_16x16x4_f64 over the NT(NT+1)/2 upper-triangle 16x16 tile pairs
+//   (NT = ceil(p/16): p = 96 needs 21 pairs, not the 28 a padded [1, x, y] block would), while the
+//   border (sums of x and y, x'y, y'y, row count) is accumulated on the VALU from the same
+//   fragments.  Waves: 2 pair groups x 2 row halves; partial sums are combined in a fixed order,
+//   so results are deterministic.  The shift is found in the first block holding a usable row;
+//   later blocks subtract it while staging.
 // Algorithmic work per segment: rows * (p+2)(p+3) flops over 8(p+1) B per row.
 #include "afm_internal.h"
 
@@ -46,161 +49,252 @@ struct GramArgs {
     double* shift;           // [nseg][p2]
 };
 
-__device__ __forceinline__ int pair_I(int q, int nt) {
-    int I = 0;
-    while (q >= nt - I) { q -= nt - I; ++I; }
-    return I;
-}
-__device__ __forceinline__ int pair_J(int q, int nt) {
-    int I = 0;
-    while (q >= nt - I) { q -= nt - I; ++I; }
-    return I + q;
-}
+// upper-triangle tile pairs in J-major order: q -> (I, J), I <= J
+template <int NT>
+struct PairTab {
+    static constexpr int NP = NT * (NT + 1) / 2;
+    int I[NP], J[NP];
+    constexpr PairTab() : I(), J() {
+        int q = 0;
+        for (int j = 0; j < NT; ++j)
+            for (int i = 0; i <= j; ++i) { I[q] = i; J[q] = j; ++q; }
+    }
+};
 
-constexpr int kPer = ((kMaxF - 1) * kRows + kThreads - 1) / kThreads;   // staged values per thread
+// pairs [Q0, Q1) of the table (group 0: the first half, group 1: the rest -- it touches every
+// tile, so it also owns the border sums)
+template <int NT, int GRP>
+struct Group {
+    static constexpr int NP = NT * (NT + 1) / 2;
+    static constexpr int Q0 = GRP == 0 ? 0 : NP / 2;
+    static constexpr int Q1 = GRP == 0 ? NP / 2 : NP;
+    static constexpr int NQ = Q1 - Q0;
+    static constexpr int NQA = NQ > 0 ? NQ : 1;
+    static constexpr int TMAX = GRP == 0 ? (NQ > 0 ? PairTab<NT>().J[Q1 - 1] + 1 : 0) : NT;
+};
 
-__global__ __launch_bounds__(kThreads) void gram_kernel(GramArgs g) {
-    __shared__ double tile[kMaxF][kRS];
-    __shared__ double sh[kMaxF];
-    __shared__ int colsL[kMaxF];
-    __shared__ int rowok[kRows];
-    __shared__ int flags[2];               // [0] shift set, [1] tile has a usable row
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int p = g.p, p2 = p + 2;
-    const int nt = (p2 + 15) / 16;
-    const int npairs = nt * (nt + 1) / 2;
-    // split 4 waves over tile pairs (WP) x row k-steps (WK)
-    const int WP = npairs >= 8 ? 4 : (npairs >= 3 ? 2 : 1);
-    const int WK = 4 / WP;
-    const int wp = wave % WP, wk = wave / WP;
+template <int NT>
+struct GramSmem {
+    static constexpr int NF = NT * 16;
+    static constexpr int NP = NT * (NT + 1) / 2;
+    // tile rows: the staged block (x features 0..NF-1 zero padded, y at row NF), reused by the
+    // epilogue for the partial sums of the second row half (pairs x 256 + border x 64)
+    static constexpr int RED = NP * 256 + (2 * NT + 3) * 64;
+    static constexpr int ROWS = (NF + 2) * kRS >= RED ? NF + 2 : (RED + kRS - 1) / kRS;
+    double tile[ROWS][kRS];
+    double shs[NF + 1];
+    int rowbit[kRows];             // mask bit of row r0 + a
+    int rowbad[kRows];             // == block counter: some value of the row is non-finite
+    int64_t coff[NF + 4];          // element offset of staged feature f (f > p: y again)
+    int lrow[NF + 4];              // tile row of staged feature f (f > p: the dump row NF + 1)
+    int found;
+};
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// One wave of pair group GRP, row half kh.  All four waves run the same barrier sequence.
+template <int NT, int GRP>
+__device__ void gram_body(const GramArgs& g, GramSmem<NT>& sm, const int wave, const int lane) {
+    using G = Group<NT, GRP>;
+    constexpr int NF = NT * 16;
+    constexpr int KPER = ((NF + 1) * kRows + kThreads - 1) / kThreads;
+    constexpr PairTab<NT> tab{};
+    const int kh = wave & 1;
+    const int p = g.p;
     const int64_t seg = g.seg0 + blockIdx.x;
     const int64_t rowbase = seg * g.seg_stride;
-    const int nstage = (p + 1) * kRows;
+    const int tid = threadIdx.x;
 
-    for (int i = tid; i < kMaxF * kRS; i += kThreads) (&tile[0][0])[i] = 0.0;
-    if (tid < kMaxF) sh[tid] = 0.0;
-    if (tid < p + 1) colsL[tid] = tid < p ? g.cols[tid] : g.ycol;
-    if (tid == 0) flags[0] = 0;
-    // this wave's tile pairs
-    int pI[kMaxTiles], pJ[kMaxTiles];
-#pragma unroll
-    for (int q = 0; q < kMaxTiles; ++q) {
-        const int pq = wp + q * WP;
-        pI[q] = pq < npairs ? pair_I(pq, nt) : 0;
-        pJ[q] = pq < npairs ? pair_J(pq, nt) : 0;
-    }
-    d4 acc[kMaxTiles];
-#pragma unroll
-    for (int q = 0; q < kMaxTiles; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
-    __syncthreads();
-
-    // register prefetch of one 64-row tile of features 1..p+1
-    double pre[kPer];
+    // staging slots: element j of this thread = feature f = wave + 4 j (wave-uniform; f == p is
+    // y, f > p re-reads y into a dump row), row a = lane.  Rows past the segment (or the long
+    // design's row_limit) are clamped to its last row and masked out by rowbit.
+    double pre[KPER];
+    int64_t rmax = g.seg_rows - 1;
+    if (g.row_limit >= 0 && g.row_limit - 1 - rowbase < rmax) rmax = g.row_limit - 1 - rowbase;
     auto prefetch = [&](int64_t r0) {
+        int64_t r = r0 + lane;
+        r = r < rmax ? r : rmax;
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = tid + j * kThreads;
-            double x = 0.0;
-            if (i < nstage) {
-                const int f = 1 + (i >> 6), a = i & (kRows - 1);
-                const int64_t r = r0 + a;
-                bool in = r < g.seg_rows;
-                if (g.row_limit >= 0) in = in && (rowbase + r < g.row_limit);
-                if (in) x = g.base[(int64_t)colsL[f - 1] * g.col_stride + rowbase + r];
-            }
-            pre[j] = x;
-        }
+        for (int j = 0; j < KPER; ++j) pre[j] = g.base[sm.coff[wave + 4 * j] + r];
     };
     prefetch(0);
 
-    for (int64_t r0 = 0; r0 < g.seg_rows; r0 += kRows) {
-        // ---- row mask of rows r0..r0+63, stage the prefetched values ----
+    d4 acc[G::NQA];
+#pragma unroll
+    for (int q = 0; q < G::NQA; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    double bs[NT], bc[NT];          // border (GRP 1): per lane sum x, sum x*y
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { bs[t] = 0.0; bc[t] = 0.0; }
+    double sy = 0.0, syy = 0.0, nn = 0.0;
+    const int fi = lane & 15, kk = lane >> 4;
+
+    bool have_shift = false;
+    int blk = 0;
+    for (int64_t r0 = 0; r0 < g.seg_rows; r0 += kRows, ++blk) {
+        // ---- stage: mask bits, values (minus the shift once known), non-finite flags ----
         if (tid < kRows) {
-            int64_t r = r0 + tid;
+            const int64_t r = r0 + tid;
             bool ok = r < g.seg_rows;
             if (ok && g.row_limit >= 0) ok = rowbase + r < g.row_limit;
-            if (ok && g.bits) {
-                u64 w = g.bits[(seg >> 6) * g.seg_stride + r];
-                ok = (w >> (seg & 63)) & 1ull;
-            }
-            rowok[tid] = ok ? 1 : 0;
+            if (ok && g.bits) ok = (g.bits[(seg >> 6) * g.seg_stride + r] >> (seg & 63)) & 1ull;
+            sm.rowbit[tid] = ok ? 1 : 0;
         }
-        __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-            const int i = tid + j * kThreads;
-            if (i < nstage) {
-                const int f = 1 + (i >> 6), a = i & (kRows - 1);
-                const double x = pre[j];
-                if (rowok[a] && !__builtin_isfinite(x)) rowok[a] = 0;   // benign race: stores 0
-                tile[f][a] = x;
-            }
+        for (int j = 0; j < KPER; ++j) {
+            const int lr = sm.lrow[wave + 4 * j];
+            const double x = pre[j];
+            if (!__builtin_isfinite(x)) sm.rowbad[lane] = blk;       // benign race: same value
+            sm.tile[lr][lane] = x - sm.shs[lr];                       // shs = 0 until found
         }
         __syncthreads();
-        if (r0 + kRows < g.seg_rows) prefetch(r0 + kRows);           // in flight during MFMA
-        if (wave == 0) {
-            u64 m = __ballot(rowok[lane] != 0);
-            if (lane == 0) flags[1] = m != 0ull;
-            if (m != 0ull && flags[0] == 0) {
-                int a0 = __builtin_ctzll(m);
-                for (int f = 1 + lane; f < p2; f += 64) sh[f] = tile[f][a0];
-                if (lane == 0) flags[0] = 1;
-            }
-        }
-        __syncthreads();
-        if (!flags[1]) continue;                   // uniform: nothing usable in this tile
-        for (int i = tid; i < p2 * kRows; i += kThreads) {
-            int f = i >> 6, a = i & (kRows - 1);
-            double v = 0.0;
-            if (rowok[a]) v = (f == 0) ? 1.0 : tile[f][a] - sh[f];
-            tile[f][a] = v;
-        }
-        __syncthreads();
-        // ---- MFMA: acc[pair] += Z[:, I]^T Z[:, J] over this wave's k-steps ----
-        const int fi = lane & 15, kk = lane >> 4;
-        for (int ks = wk; ks < kRows / 4; ks += WK) {
-            const int a = ks * 4 + kk;
-#pragma unroll
-            for (int q = 0; q < kMaxTiles; ++q) {
-                if (wp + q * WP < npairs) {
-                    const double va = tile[pI[q] * 16 + fi][a];
-                    const double vb = tile[pJ[q] * 16 + fi][a];
-                    acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(va, vb, acc[q], 0, 0, 0);
+        if (r0 + kRows < g.seg_rows) prefetch(r0 + kRows);        // in flight during the MFMAs
+        if (!have_shift) {
+            // first block with a usable row: its first usable row becomes the shift
+            if (wave == 0) {
+                const u64 m = __ballot(sm.rowbit[lane] && sm.rowbad[lane] != blk);
+                if (m != 0ull) {
+                    const int a0 = __builtin_ctzll(m);
+                    for (int f = lane; f <= NF; f += 64) sm.shs[f] = (f < p || f == NF) ? sm.tile[f][a0] : 0.0;
+                    if (lane == 0) sm.found = 1;
                 }
             }
+            __syncthreads();
+            const bool fnd = sm.found != 0;
+            __syncthreads();
+            if (!fnd) continue;                                    // uniform
+            have_shift = true;
+#pragma unroll
+            for (int j = 0; j < KPER; ++j) {
+                const int lr = sm.lrow[wave + 4 * j];
+                sm.tile[lr][lane] = sm.tile[lr][lane] - sm.shs[lr];
+            }
+            __syncthreads();
+        }
+        // ---- MFMA over this wave's k-steps: kh, kh + 2, .. ----
+#pragma unroll 2
+        for (int it = 0; it < kRows / 8; ++it) {
+            const int a = (kh + 2 * it) * 4 + kk;
+            const bool ok = sm.rowbit[a] && sm.rowbad[a] != blk;
+            double fr[NT];
+#pragma unroll
+            for (int t = 0; t < G::TMAX; ++t) fr[t] = ok ? sm.tile[t * 16 + fi][a] : 0.0;
+            if (GRP == 1) {
+                const double yv = ok ? sm.tile[NF][a] : 0.0;
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    bs[t] = bs[t] + fr[t];
+                    bc[t] = __builtin_fma(fr[t], yv, bc[t]);
+                }
+                sy = sy + yv;
+                syy = __builtin_fma(yv, yv, syy);
+                nn = nn + (ok ? 1.0 : 0.0);
+            }
+#pragma unroll
+            for (int q = 0; q < G::NQ; ++q)
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[tab.I[G::Q0 + q]],
+                                                              fr[tab.J[G::Q0 + q]], acc[q], 0, 0, 0);
         }
         __syncthreads();
     }
 
-    // ---- combine the WK row-groups in a fixed order, write G' (full symmetric) ----
+    // ---- epilogue: row half 1 parks its partials, row half 0 adds them (fixed order) ----
+    const int p2 = p + 2;
     double* out = g.gram + (int64_t)blockIdx.x * p2 * p2;
-    double* red = &tile[0][0];               // reuse: [WK][WP][kMaxTiles][64 lanes][4]
-    auto slot = [&](int k_, int q_, int r_) {
-        return (((k_ * WP + wp) * kMaxTiles + q_) * 64 + lane) * 4 + r_;
-    };
-    if (WK > 1) {
-        for (int q = 0; q < kMaxTiles; ++q)
-            for (int r = 0; r < 4; ++r) red[slot(wk, q, r)] = acc[q][r];
-        __syncthreads();
+    double* red = &sm.tile[0][0] + (GRP == 0 ? 0 : Group<NT, 0>::NQ * 256);
+    double* rb = &sm.tile[0][0] + GramSmem<NT>::NP * 256;          // border partials
+    if (kh == 1) {
+#pragma unroll
+        for (int q = 0; q < G::NQ; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[(q * 4 + r) * 64 + lane] = acc[q][r];
+        if (GRP == 1) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) { rb[t * 64 + lane] = bs[t]; rb[(NT + t) * 64 + lane] = bc[t]; }
+            rb[(2 * NT) * 64 + lane] = sy;
+            rb[(2 * NT + 1) * 64 + lane] = syy;
+            rb[(2 * NT + 2) * 64 + lane] = nn;
+        }
     }
-    if (wk == 0) {
-        for (int q = 0; q < kMaxTiles; ++q) {
-            const int pq = wp + q * WP;
-            if (pq >= npairs) continue;
-            const int I = pI[q], J = pJ[q];
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+        for (int q = 0; q < G::NQ; ++q) {
+            const int I = tab.I[G::Q0 + q], J = tab.J[G::Q0 + q];
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
-                double v = acc[q][r];
-                for (int k = 1; k < WK; ++k) v += red[slot(k, q, r)];
+                const double v = acc[q][r] + red[(q * 4 + r) * 64 + lane];
                 const int row = I * 16 + (lane >> 4) + 4 * r;   // f64 MFMA C/D layout
                 const int col = J * 16 + (lane & 15);
-                if (row < p2 && col < p2) {
-                    out[row * p2 + col] = v;
-                    out[col * p2 + row] = v;
+                if (row < p && col < p) {
+                    out[(1 + row) * p2 + 1 + col] = v;
+                    out[(1 + col) * p2 + 1 + row] = v;
                 }
             }
         }
+        if (GRP == 1) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                rb[t * 64 + lane] = bs[t] + rb[t * 64 + lane];
+                rb[(NT + t) * 64 + lane] = bc[t] + rb[(NT + t) * 64 + lane];
+            }
+            rb[(2 * NT) * 64 + lane] = sy + rb[(2 * NT) * 64 + lane];
+            rb[(2 * NT + 1) * 64 + lane] = syy + rb[(2 * NT + 1) * 64 + lane];
+            rb[(2 * NT + 2) * 64 + lane] = nn + rb[(2 * NT + 2) * 64 + lane];
+            lds_fence();
+            // lane group kk holds rows == kk (mod 4): sum the 4 groups in order
+            for (int f = lane; f < p; f += 64) {
+                const int t = f >> 4, c = f & 15;
+                double s = 0.0, x = 0.0;
+                for (int k4 = 0; k4 < 4; ++k4) {
+                    s = s + rb[t * 64 + k4 * 16 + c];
+                    x = x + rb[(NT + t) * 64 + k4 * 16 + c];
+                }
+                out[1 + f] = s;
+                out[(1 + f) * p2] = s;
+                out[(1 + f) * p2 + p + 1] = x;
+                out[(p + 1) * p2 + 1 + f] = x;
+            }
+            if (lane == 0) {
+                double s = 0.0, q = 0.0, n = 0.0;
+                for (int k4 = 0; k4 < 4; ++k4) {
+                    s = s + rb[(2 * NT) * 64 + k4 * 16];
+                    q = q + rb[(2 * NT + 1) * 64 + k4 * 16];
+                    n = n + rb[(2 * NT + 2) * 64 + k4 * 16];
+                }
+                out[0] = n;
+                out[p + 1] = s;
+                out[(p + 1) * p2] = s;
+                out[(p + 1) * p2 + p + 1] = q;
+            }
+        }
     }
-    if (tid < p2) g.shift[(int64_t)blockIdx.x * p2 + tid] = sh[tid];
+}
+
+template <int NT, int MINW>
+__global__ __launch_bounds__(kThreads, MINW) void gram_kernel(GramArgs g) {
+    constexpr int NF = NT * 16;
+    __shared__ GramSmem<NT> sm;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int p = g.p;
+    const int64_t rowbase = (g.seg0 + blockIdx.x) * g.seg_stride;
+    for (int i = tid; i < GramSmem<NT>::ROWS * kRS; i += kThreads) (&sm.tile[0][0])[i] = 0.0;
+    for (int i = tid; i < NF + 4; i += kThreads) {
+        if (i <= NF) sm.shs[i] = 0.0;
+        const int c = i < p ? g.cols[i] : g.ycol;
+        sm.coff[i] = (int64_t)c * g.col_stride + rowbase;
+        sm.lrow[i] = i < p ? i : (i == p ? NF : NF + 1);
+    }
+    if (tid < kRows) sm.rowbad[tid] = -1;
+    if (tid == 0) sm.found = 0;
+    __syncthreads();
+    if (wave < 2) gram_body<NT, 0>(g, sm, wave, lane);
+    else gram_body<NT, 1>(g, sm, wave, lane);
+    const int p2 = p + 2;
+    if (tid < p2) {
+        const double v = tid == 0 ? 0.0 : (tid <= p ? sm.shs[tid - 1] : sm.shs[NF]);
+        g.shift[(int64_t)blockIdx.x * p2 + tid] = v;
+    }
 }
 
 // ---- per-segment OLS from the shifted Gram -------------------------------------------------
@@ -469,7 +563,17 @@ extern "C" int afm_xs_gram_f64(afm_ctx* ctx, const double* base, int64_t col_str
     if (nseg == 0) return AFM_OK;
     GramArgs g{base, col_stride, seg_stride, seg_rows, row_limit, cols, ycol, p, bits, seg0, gram,
                shift};
-    hipLaunchKernelGGL(gram_kernel, dim3((unsigned)nseg), dim3(kThreads), 0, ctx->stream, g);
+    const int nt = (p + 15) / 16;
+    const dim3 grid((unsigned)nseg), blk(kThreads);
+    switch (nt) {
+        case 1: hipLaunchKernelGGL((gram_kernel<1, 2>), grid, blk, 0, ctx->stream, g); break;
+        case 2: hipLaunchKernelGGL((gram_kernel<2, 2>), grid, blk, 0, ctx->stream, g); break;
+        case 3: hipLaunchKernelGGL((gram_kernel<3, 2>), grid, blk, 0, ctx->stream, g); break;
+        case 4: hipLaunchKernelGGL((gram_kernel<4, 2>), grid, blk, 0, ctx->stream, g); break;
+        case 5: hipLaunchKernelGGL((gram_kernel<5, 2>), grid, blk, 0, ctx->stream, g); break;
+        case 6: hipLaunchKernelGGL((gram_kernel<6, 2>), grid, blk, 0, ctx->stream, g); break;
+        default: hipLaunchKernelGGL((gram_kernel<7, 2>), grid, blk, 0, ctx->stream, g); break;
+    }
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
