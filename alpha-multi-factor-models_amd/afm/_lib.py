@@ -11,7 +11,8 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libafm.so")
+# AFM_LIB: an alternative build of the same library (A/B kernel variants, profiling builds)
+LIB_PATH = os.environ.get("AFM_LIB") or os.path.join(HERE, "libafm.so")
 
 P = ctypes.c_void_p
 I64 = ctypes.c_int64

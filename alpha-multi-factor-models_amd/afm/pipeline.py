@@ -94,8 +94,10 @@ class Pipeline:
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         self.ctx = _lib.Context.get(dev.index)
 
-    def step(self, events: dict | None = None):
-        """One pass of the hot path.  ``events``: optional {stage: (start, end)} CUDA events."""
+    def step(self, events: dict | None = None, only=None):
+        """One pass of the hot path.  ``events``: optional {stage: (start, end)} CUDA events.
+        ``only``: optional set of stage names to run (profiling; the others keep their last
+        results)."""
         L = _lib.lib()
         P = _lib.ptr
         chk = _lib.check
@@ -107,46 +109,57 @@ class Pipeline:
             if events is not None:
                 events[stage][which].record()
 
-        mark("factors", 0)
-        chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), P(g.ret1d), P(g.excess),
-                              P(g.vbits), P(self.out), P(self.nanfree), P(self.finite)), "factors")
-        mark("factors", 1)
-        mark("xs_gram", 0)
-        chk(L.afm_xs_gram_f64(h, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p, c.ycol,
-                              P(self.finite), 0, T, P(self.gram), P(self.shift)), "xs_gram")
-        mark("xs_gram", 1)
-        mark("xs_solve", 0)
-        chk(L.afm_ols_solve_f64(h, P(self.gram), P(self.shift), p, T, c.tol, P(self.beta),
-                                P(self.nobs), P(self.rank)), "ols_solve")
-        chk(L.afm_fama_macbeth_f64(h, P(self.beta), P(self.rank), T, p + 1, P(self.fm_mean),
-                                   P(self.fm_t)), "fama_macbeth")
-        mark("xs_solve", 1)
-        mark("pooled_ols", 0)
-        chk(L.afm_pool_moments_f64(h, P(self.gram), P(self.shift), p, self.t_test,
-                                   P(self.pool_g), P(self.pool_s)), "pool")
-        chk(L.afm_ols_solve_f64(h, P(self.pool_g), P(self.pool_s), p, 1, c.tol,
-                                P(self.pool_beta), P(self.pool_n), P(self.pool_rank)), "pool_solve")
-        mark("pooled_ols", 1)
-        mark("predict", 0)
-        chk(L.afm_predict_f64(h, P(self.out), T * lda, lda, self.t_test, T - self.t_test,
-                              P(self.cols), p, P(self.pool_beta), 0, P(self.finite), c.ycol,
-                              P(self.pred)), "predict")
-        mark("predict", 1)
-        mark("rebalance", 0)
-        r = self.reb
-        chk(L.afm_rebalance_f64(h, T, g.A, lda, P(self.rdates), self.nd, P(self.pred),
-                                P(g.tbits), P(self.out[c.ycol]), P(g.vbits), 0, T,
-                                -1 if c.window is None else int(c.window), P(g.close),
-                                P(self.out[N_FACTORS - 1]), c.top_n, c.lo, c.hi, P(r["k"]),
-                                P(r["books"]), P(r["weights"]), P(r["sums"]), P(r["upos"]),
-                                P(r["usize"]), P(r["status"])), "rebalance")
-        mark("rebalance", 1)
-        mark("pnl", 0)
-        q = self.pnl
-        chk(L.afm_pnl_scan_f64(h, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]), P(r["upos"]),
-                               P(r["usize"]), 100000000.0, c.rate, P(q["value"]),
-                               P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])), "pnl")
-        mark("pnl", 1)
+        def on(stage):
+            return only is None or stage in only
+
+        if on("factors"):
+            mark("factors", 0)
+            chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), P(g.ret1d), P(g.excess),
+                                  P(g.vbits), P(self.out), P(self.nanfree), P(self.finite)), "factors")
+            mark("factors", 1)
+        if on("xs_gram"):
+            mark("xs_gram", 0)
+            chk(L.afm_xs_gram_f64(h, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p, c.ycol,
+                                  P(self.finite), 0, T, P(self.gram), P(self.shift)), "xs_gram")
+            mark("xs_gram", 1)
+        if on("xs_solve"):
+            mark("xs_solve", 0)
+            chk(L.afm_ols_solve_f64(h, P(self.gram), P(self.shift), p, T, c.tol, P(self.beta),
+                                    P(self.nobs), P(self.rank)), "ols_solve")
+            chk(L.afm_fama_macbeth_f64(h, P(self.beta), P(self.rank), T, p + 1, P(self.fm_mean),
+                                       P(self.fm_t)), "fama_macbeth")
+            mark("xs_solve", 1)
+        if on("pooled_ols"):
+            mark("pooled_ols", 0)
+            chk(L.afm_pool_moments_f64(h, P(self.gram), P(self.shift), p, self.t_test,
+                                       P(self.pool_g), P(self.pool_s)), "pool")
+            chk(L.afm_ols_solve_f64(h, P(self.pool_g), P(self.pool_s), p, 1, c.tol,
+                                    P(self.pool_beta), P(self.pool_n), P(self.pool_rank)), "pool_solve")
+            mark("pooled_ols", 1)
+        if on("predict"):
+            mark("predict", 0)
+            chk(L.afm_predict_f64(h, P(self.out), T * lda, lda, self.t_test, T - self.t_test,
+                                  P(self.cols), p, P(self.pool_beta), 0, P(self.finite), c.ycol,
+                                  P(self.pred)), "predict")
+            mark("predict", 1)
+        if on("rebalance"):
+            mark("rebalance", 0)
+            r = self.reb
+            chk(L.afm_rebalance_f64(h, T, g.A, lda, P(self.rdates), self.nd, P(self.pred),
+                                    P(g.tbits), P(self.out[c.ycol]), P(g.vbits), 0, T,
+                                    -1 if c.window is None else int(c.window), P(g.close),
+                                    P(self.out[N_FACTORS - 1]), c.top_n, c.lo, c.hi, P(r["k"]),
+                                    P(r["books"]), P(r["weights"]), P(r["sums"]), P(r["upos"]),
+                                    P(r["usize"]), P(r["status"])), "rebalance")
+            mark("rebalance", 1)
+        if on("pnl"):
+            mark("pnl", 0)
+            r = self.reb
+            q = self.pnl
+            chk(L.afm_pnl_scan_f64(h, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]), P(r["upos"]),
+                                   P(r["usize"]), 100000000.0, c.rate, P(q["value"]),
+                                   P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])), "pnl")
+            mark("pnl", 1)
 
     def summary(self) -> dict:
         """Host copies of the headline results (after a synchronize)."""

@@ -5,24 +5,33 @@
 // [ceil(T/64)][lda] uint64, output planes [98][T][lda].
 //
 // Kernel design (MI355X):
-//  * One workgroup = 64 assets (one per lane) x 16 waves.  Every wave walks the SAME 64 assets
-//    through time; each wave owns a fixed, compile-time set of indicator "jobs" whose state
-//    (Kahan sums, Welford moments, ewm weights, cumsums) lives in its registers for the whole
-//    series.  pandas' rolling/ewm kernels are sequential recurrences whose rounding depends on
-//    the full history (Kahan compensation is never reset), so bit-exactness requires exactly
-//    this: a sequential scan per asset, parallel over assets x job groups.
+//  * pandas' rolling/ewm kernels are sequential recurrences whose rounding depends on the full
+//    history (Kahan compensations are never reset), so bit-exactness requires a sequential scan
+//    per asset.  Parallelism = assets (one per lane) x indicator jobs (one job set per wave).
+//  * One workgroup = one 64-asset block: 15 job waves (balanced by the VALU count of each job's
+//    compiled step, and so that the four SIMDs carry equal totals) + 1 loader wave; the kernel
+//    is VALU-issue-bound (~86% of each SIMD's cycles).  An LDS ring holds the last kRing
+//    present observations of close and volume per lane.  (AFM_FP_TYPES=3 splits a block's jobs
+//    over 3 workgroups; measured on MI355X, workgroups of 78 KB LDS do not co-reside -- the
+//    two-per-CU limit was between 52 and 56 KB -- so that layout runs in two rounds and is
+//    slower at 10k assets; kept for few-block shards.)
+//  * The loader wave is the only one that reads global memory: it fills the ring one chunk
+//    ahead of the scan and publishes each chunk's presence bits.  The job waves only store, so
+//    they never wait on vmcnt (loads and stores share the counter on gfx950: a wave that both
+//    prefetches and streams stores must drain its stores before it can use a prefetched value).
 //  * Windows are positional over each asset's PRESENT days (holes and listing gaps do not count,
-//    No-talib.py:5-6).  A shared LDS ring holds the last 128 present observations of close and
-//    volume per lane (128 KB), indexed by the lane's observation count; 128 >= 57 (ACCEL_56
-//    lookback) + 64 (chunk) + 1.  Derived series (returns, volume change, vol*close, up-days)
-//    are recomputed from the ring with the same IEEE ops pandas uses.
-//  * Time advances in chunks of 64 calendar days = one presence word.  Per chunk: the 16 waves
-//    write the chunk's close/volume (prefetched into registers during the previous chunk) into
-//    the ring (4 days each), barrier, every wave scans the 64 days for its jobs and streams
-//    its output columns as coalesced 512-B row stores, barrier.  Absent cells are not written.
-//  * dropna bookkeeping: each wave ORs a per-lane "some output NaN at day s" bit into an LDS
-//    word; after the chunk wave 0 stores nanfree = present & ~nanmask.
-//  * -ffp-contract=off + IEEE div/sqrt: every value rounds exactly as numpy/pandas on x86-64.
+//    No-talib.py:5-6); the ring is indexed by the lane's observation count (mod kRing).
+//  * Time advances in chunks of kChunk = 8 calendar days, one barrier per chunk: the job waves
+//    step their jobs over chunk c's present days and stream their output columns as coalesced
+//    512-B row stores while the loader writes chunk c+1 into the ring and issues the loads of
+//    chunk c+2.  Absent cells are not written.
+//  * Divisions by an observation count (window means, Welford updates, variances, PSY) use a
+//    correctly rounded reciprocal table and one Markstein correction -- the exactly rounded
+//    quotient for every integer divisor <= 64 (FMA; no contraction elsewhere); ewm skips its
+//    division by (old + alpha) == 1.0 exactly.  Other divisions are IEEE.
+//  * dropna bookkeeping: each wave ORs its per-lane "some output NaN / non-finite at day s" bits
+//    into LDS words; at each 64-day word the workgroup stores its type's partial masks, and
+//    masks_kernel combines the kTypes partials into nanfree / finite.
 //
 // Algorithmic traffic per present asset-day: 32 B of inputs read + 98 x 8 B written = 816 B.
 #include "afm_internal.h"
@@ -33,12 +42,27 @@ namespace afm {
 namespace {
 
 constexpr int kLanes = 64;
-constexpr int kRing = 128;
-constexpr int kChunk = 64;
-constexpr int kWaves = 16;
-constexpr int kLoadSteps = kChunk / kWaves;  // 4 days loaded into the ring per wave per chunk
+constexpr int kChunk = 8;
+// the loader fills chunk c+1 while the job waves scan chunk c: the ring must hold the scan's
+// lookback (57) plus two chunks
+#ifdef AFM_FP_RING
+constexpr int kRing = AFM_FP_RING;     // experiments only
+#else
+constexpr int kRing = 57 + 2 * kChunk + 1;
+#endif
+#ifndef AFM_FP_TYPES
+#define AFM_FP_TYPES 1
+#endif
+constexpr int kTypes = AFM_FP_TYPES;        // workgroups (job-set types) per 64-asset block
+constexpr int kJobWaves = 15 / kTypes;      // job waves per workgroup
+constexpr int kWaves = kJobWaves + 1;       // + one loader wave (the last)
+constexpr int kMinWavesPerSimd = kTypes == 1 ? 4 : 3;
 
 typedef unsigned long long u64;
+#ifdef AFM_FP_PROFILE
+// profiling build only: per-(workgroup, wave) cycles spent in the chunk loop
+__device__ long long g_wave_cycles[1 << 16];
+#endif
 // explicit address spaces: the per-wave functions are not inlined, and generic (flat) pointers
 // would turn every ring read into a flat_load that waits on all outstanding global stores
 #define LDS __attribute__((address_space(3)))
@@ -57,9 +81,23 @@ __device__ __forceinline__ double zsqrt(double x) { return x < 0 ? 0.0 : __built
 struct Smem {
     double c[kRing][kLanes];   // close ring (by observation index mod kRing)
     double v[kRing][kLanes];   // volume ring
+    double rtab[128];          // rtab[n] = 1.0 / n (IEEE), rtab[0] = +inf; indexed n & 127
+    int cbyte[2][kLanes];      // presence bits of chunk c (parity c & 1), written by the loader
     u64 nanmask[kLanes];
     u64 badmask[kLanes];       // some factor non-finite (NaN or +-inf)
 };
+
+// x / n exactly rounded for integer 0 <= n <= 64 (Markstein: r = RN(1/n), q0 = RN(x r),
+// q = RN(q0 + (x - q0 n) r)); zero and non-finite quotients pass through (keeps -0, inf, NaN).
+// Out-of-range n (only in discarded lanes of the branch-free updates) reads a defined entry.
+__device__ __forceinline__ double div_n(const LDS Smem* sm, double x, int n) {
+    const double d = (double)n;
+    const double r = sm->rtab[n & 127];
+    const double q0 = x * r;
+    const double e = __builtin_fma(-q0, d, x);
+    const double q1 = __builtin_fma(e, r, q0);
+    return (q0 == 0.0 || !__builtin_isfinite(q0)) ? q0 : q1;
+}
 
 struct Args {
     int64_t T, lda, plane;     // plane = T * lda
@@ -67,30 +105,36 @@ struct Args {
     const GLB double* volume;
     const GLB uint64_t* vbits;
     GLB double* out;
-    GLB uint64_t* nanfree;
-    GLB uint64_t* finite;      // optional
+    GLB uint64_t* nanpart;     // [kTypes][nch][lda] per-type "some output NaN" bits
+    GLB uint64_t* badpart;     // [kTypes][nch][lda] per-type "some output non-finite" bits
 };
 
-// Per-lane view of one (asset, present day) step.
+// Per-lane view of one (asset, present day) step.  Lookback L reads observation p - L.
 struct Step {
     const LDS Smem* sm;
     GLB double* out;
     int64_t plane, cell;
-    int lane, p;               // p = index of this observation in the asset's series
+    int lane, p, pm;           // p = observation index of this day, pm = p mod kRing
     bool anynan, anybad;
-    __device__ __forceinline__ double C(int q) const { return sm->c[q & (kRing - 1)][lane]; }
-    __device__ __forceinline__ double V(int q) const { return sm->v[q & (kRing - 1)][lane]; }
+    double r0;                 // ret(p), computed once per step (ret(0))
+    __device__ __forceinline__ int slot(int L) const { return pm - L + (pm < L ? kRing : 0); }
+    __device__ __forceinline__ double C(int L) const { return sm->c[slot(L)][lane]; }
+    __device__ __forceinline__ double V(int L) const { return sm->v[slot(L)][lane]; }
+    __device__ __forceinline__ double div(double x, int n) const { return div_n(sm, x, n); }
     __device__ __forceinline__ void put(int col, double x) {
         out[col * plane + cell] = x;
         anynan |= (x != x);
         anybad |= !__builtin_isfinite(x);
     }
-    // close.pct_change() at q, with the window kernels' inf -> NaN (_prep_values)
-    __device__ __forceinline__ double ret(int q) const {
-        return q >= 1 ? C(q) / C(q - 1) - 1 : qnan();
+    // close.pct_change() at lookback L, with the window kernels' inf -> NaN (_prep_values)
+    __device__ __forceinline__ double ret(int L) const {
+        if (L == 0) return r0;
+        const double r = C(L) / C(L + 1) - 1;
+        return p - L >= 1 ? r : qnan();
     }
-    __device__ __forceinline__ double volchg(int q) const {
-        return q >= 1 ? V(q) / V(q - 1) - 1 : qnan();
+    __device__ __forceinline__ double volchg(int L) const {
+        const double g = V(L) / V(L + 1) - 1;
+        return p - L >= 1 ? g : qnan();
     }
 };
 
@@ -126,9 +170,9 @@ struct RollMean {
             neg -= __builtin_signbit(x) ? 1 : 0;
         }
     }
-    __device__ __forceinline__ double result(int minp) const {
+    __device__ __forceinline__ double result(const Step& s, int minp) const {
         if (nobs >= minp && nobs > 0) {
-            double r = sum / (double)nobs;
+            double r = s.div(sum, nobs);
             if (same >= nobs) r = prev;
             else if (neg == 0 && r < 0) r = 0.0;
             else if (neg == nobs && r > 0) r = 0.0;
@@ -140,31 +184,31 @@ struct RollMean {
 
 // roll_var, ddof = 1: Welford with Kahan-compensated mean; the remove runs before the add.
 struct RollVar {
-    double mean, ssq, nobs, cadd, crem, prev;
-    int same;
+    double mean, ssq, cadd, crem, prev;
+    int nobs, same;
     __device__ __forceinline__ void init() {
-        mean = ssq = nobs = cadd = crem = 0.0;
+        mean = ssq = cadd = crem = 0.0;
         prev = qnan();
-        same = 0;
+        nobs = same = 0;
     }
-    __device__ __forceinline__ void add(double x) {
+    __device__ __forceinline__ void add(const Step& s, double x) {
         if (!__builtin_isnan(x)) {
             nobs = nobs + 1;
             same = (x == prev) ? same + 1 : 1;
             prev = x;
             double pm = mean - cadd, y = x - cadd, t = y - mean;
             cadd = t + mean - y;
-            mean = (nobs != 0) ? mean + t / nobs : 0.0;
+            mean = mean + s.div(t, nobs);
             ssq = ssq + (x - pm) * (x - mean);
         }
     }
-    __device__ __forceinline__ void remove(double x) {
+    __device__ __forceinline__ void remove(const Step& s, double x) {
         if (!__builtin_isnan(x)) {
             nobs = nobs - 1;
             if (nobs != 0) {
                 double pm = mean - crem, y = x - crem, t = y - mean;
                 crem = t + mean - y;
-                mean = mean - t / nobs;
+                mean = mean - s.div(t, nobs);
                 ssq = ssq - (x - pm) * (x - mean);
             } else {
                 mean = 0.0;
@@ -172,9 +216,9 @@ struct RollVar {
             }
         }
     }
-    __device__ __forceinline__ double result(int minp) const {
-        if (nobs >= (double)minp && nobs > 1.0)
-            return (nobs == 1.0 || (double)same >= nobs) ? 0.0 : ssq / (nobs - 1.0);
+    __device__ __forceinline__ double result(const Step& s, int minp) const {
+        if (nobs >= minp && nobs > 1)
+            return (same >= nobs) ? 0.0 : s.div(ssq, nobs - 1);
         return qnan();
     }
 };
@@ -182,6 +226,8 @@ struct RollVar {
 // ewm(adjust=False, ignore_na=False).mean(), minp = 1.  wtd starts NaN / old = 1, which
 // reproduces pandas' special first element exactly.  pandas emits wtd once nobs >= 1; wtd is
 // NaN exactly until the first observation, so the emitted value is wtd itself.
+// (old + alpha) is 1.0 exactly after every observed step for the spans/coms used here; the
+// division by it is then the identity and is skipped (bit-identical).
 struct Ewm {
     double wtd, old;
     __device__ __forceinline__ void init() {
@@ -194,8 +240,10 @@ struct Ewm {
             old *= owf;
             if (obs) {
                 if (wtd != cur) {
-                    wtd = old * wtd + nw * cur;
-                    wtd /= (old + nw);
+                    const double num = old * wtd + nw * cur;
+                    const double den = old + nw;
+                    wtd = num;
+                    if (den != 1.0) wtd = num / den;
                 }
                 old = 1.0;
             }
@@ -225,9 +273,9 @@ struct Sma {  // No-talib.py:9-10
     RollMean m;
     __device__ void init() { m.init(); }
     __device__ void step(Step& s) {
-        if (s.p >= W) m.remove(s.C(s.p - W));
-        m.add(s.C(s.p));
-        s.put((W - 6) / 4, m.result(W));
+        if (s.p >= W) m.remove(s.C(W));
+        m.add(s.C(0));
+        s.put((W - 6) / 4, m.result(s, W));
     }
 };
 
@@ -236,7 +284,7 @@ struct Ema {  // No-talib.py:13-14
     Ewm e;
     __device__ void init() { e.init(); }
     __device__ void step(Step& s) {
-        s.put(12 + (W - 6) / 4, e.step(s.C(s.p), SpanC<W>::owf, SpanC<W>::alpha));
+        s.put(12 + (W - 6) / 4, e.step(s.C(0), SpanC<W>::owf, SpanC<W>::alpha));
     }
 };
 
@@ -246,13 +294,14 @@ struct Vwma {  // No-talib.py:17-19
     __device__ void init() { mvc.init(); mv.init(); }
     __device__ void step(Step& s) {
         if (s.p >= W) {
-            int q = s.p - W;
-            mvc.remove(pinf(s.V(q) * s.C(q)));
-            mv.remove(s.V(q));
+            const double vq = s.V(W);
+            mvc.remove(pinf(vq * s.C(W)));
+            mv.remove(vq);
         }
-        mvc.add(pinf(s.V(s.p) * s.C(s.p)));
-        mv.add(s.V(s.p));
-        s.put(24 + (W - 6) / 4, mvc.result(W) / mv.result(W));
+        const double v0 = s.V(0);
+        mvc.add(pinf(v0 * s.C(0)));
+        mv.add(v0);
+        s.put(24 + (W - 6) / 4, mvc.result(s, W) / mv.result(s, W));
     }
 };
 
@@ -263,14 +312,14 @@ struct Bbands {  // No-talib.py:22-26
     __device__ void init() { m.init(); v.init(); }
     __device__ void step(Step& s) {
         if (s.p >= W) {
-            double x = s.C(s.p - W);
-            m.remove(x);
-            v.remove(x);
+            const double xr = s.C(W);
+            m.remove(xr);
+            v.remove(s, xr);
         }
-        double x = s.C(s.p);
+        double x = s.C(0);
         m.add(x);
-        v.add(x);
-        double ma = m.result(W), sd = zsqrt(v.result(W));
+        v.add(s, x);
+        double ma = m.result(s, W), sd = zsqrt(v.result(s, W));
         const int col = 36 + 2 * ((W - 14) / 6);
         s.put(col, ma + (2 * sd));
         s.put(col + 1, ma - (2 * sd));
@@ -282,14 +331,13 @@ struct MomAccelRocr {  // No-talib.py:35-44
     __device__ void init() {}
     __device__ void step(Step& s) {
         const int k = (W - 14) / 6;
-        double c = s.C(s.p);
-        double mom = qnan(), acc = qnan(), roc = qnan();
-        if (s.p >= W) {
-            double cw = s.C(s.p - W);
-            mom = c - cw;
-            roc = c / cw - 1;
-            if (s.p >= W + 1) acc = mom - (s.C(s.p - 1) - s.C(s.p - 1 - W));
-        }
+        double c = s.C(0);
+        const double cw = s.C(W);
+        double mom = c - cw, roc = c / cw - 1;
+        double acc = mom - (s.C(1) - s.C(1 + W));
+        mom = s.p >= W ? mom : qnan();
+        roc = s.p >= W ? roc : qnan();
+        acc = s.p >= W + 1 ? acc : qnan();
         s.put(52 + k, mom);
         s.put(60 + k, acc);
         s.put(68 + k, roc);
@@ -301,7 +349,7 @@ struct Macd {  // No-talib.py:47-50
     Ewm fast, slow;
     __device__ void init() { fast.init(); slow.init(); }
     __device__ void step(Step& s) {
-        double c = s.C(s.p);
+        double c = s.C(0);
         double f = fast.step(c, SpanC<12>::owf, SpanC<12>::alpha);
         double l = slow.step(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha);
         s.put(76 + (SLOW - 18) / 6, f - l);
@@ -313,7 +361,7 @@ struct Rsi {  // No-talib.py:53-59
     Ewm up, dn;
     __device__ void init() { up.init(); dn.init(); }
     __device__ void step(Step& s) {
-        double d = s.p >= 1 ? s.C(s.p) - s.C(s.p - 1) : qnan();
+        double d = s.p >= 1 ? s.C(0) - s.C(1) : qnan();
         bool nan = (d != d);
         double u = (nan || d >= 0) ? d : 0.0;          // delta.clip(lower=0)
         double w = -((nan || d <= 0) ? d : 0.0);       // -delta.clip(upper=0)
@@ -330,23 +378,20 @@ struct PvtObvPsy {  // No-talib.py:62-69
     __device__ void init() { pvt = 0.0; obv = 0.0; ups = 0; }
     __device__ void step(Step& s) {
         const int p = s.p;
-        double c = s.C(p), v = s.V(p);
+        double c = s.C(0), v = s.V(0);
         // PVT: nan-skipping cumsum of volume * pct_change
-        double term = p >= 1 ? v * (c / s.C(p - 1) - 1) : qnan();
+        double term = p >= 1 ? v * (c / s.C(1) - 1) : qnan();
         if (term == term) pvt = pvt + term;
         s.put(82, term == term ? pvt : qnan());
         // OBV: diff <= 0 (incl. equal closes) -> -volume, else (incl. NaN diff) +volume
-        double d = p >= 1 ? c - s.C(p - 1) : qnan();
+        double d = p >= 1 ? c - s.C(1) : qnan();
         double o = v * ((d <= 0) ? -1.0 : 1.0);
         if (o == o) obv = obv + o;
         s.put(83, o == o ? obv : qnan());
         // PSY: rolling(14) count of up-days / 14 * 100 (0/1 sums are exact)
-        ups += (p >= 1 && c > s.C(p - 1)) ? 1 : 0;
-        if (p >= 14) {
-            int q = p - 14;
-            ups -= (q >= 1 && s.C(q) > s.C(q - 1)) ? 1 : 0;
-        }
-        s.put(84, p >= 13 ? (double)ups / 14 * 100 : qnan());
+        ups += (p >= 1 && c > s.C(1)) ? 1 : 0;
+        ups -= (p >= 15 && s.C(14) > s.C(15)) ? 1 : 0;
+        s.put(84, p >= 13 ? s.div((double)ups, 14) * 100 : qnan());
     }
 };
 
@@ -355,9 +400,9 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
     RollVar v;
     __device__ void init() { v.init(); }
     __device__ double step(Step& s) {
-        if (s.p >= W) v.remove(pinf(s.ret(s.p - W)));
-        v.add(pinf(s.ret(s.p)));
-        double r = zsqrt(v.result(W));
+        if (s.p >= W) v.remove(s, pinf(s.ret(W)));
+        v.add(s, pinf(s.ret(0)));
+        double r = zsqrt(v.result(s, W));
         s.put(COL, r);
         return r;
     }
@@ -384,9 +429,9 @@ struct VolSd {  // volsd_W (No-talib.py:79-80)
     RollVar v;
     __device__ void init() { v.init(); }
     __device__ double step(Step& s) {
-        if (s.p >= W) v.remove(pinf(s.V(s.p - W)));
-        v.add(pinf(s.V(s.p)));
-        double r = zsqrt(v.result(W));
+        if (s.p >= W) v.remove(s, pinf(s.V(W)));
+        v.add(s, pinf(s.V(0)));
+        double r = zsqrt(v.result(s, W));
         s.put(COL, r);
         return r;
     }
@@ -419,36 +464,37 @@ struct Corr {
         mxy.init(); mx.init(); my.init(); vx.init(); vy.init();
         cnt = 0;
     }
-    __device__ __forceinline__ static void xy(const Step& s, int q, double& X, double& Y) {
-        double r = s.ret(q), g = s.volchg(q);
+    __device__ __forceinline__ static void xy(Step& s, int L, double& X, double& Y) {
+        double r = s.ret(L), g = s.volchg(L);
         X = pinf(r + 0 * g);
         Y = pinf(g + 0 * r);
     }
     __device__ void step(Step& s) {
         double X, Y;
         if (s.p >= W) {
-            xy(s, s.p - W, X, Y);
+            xy(s, W, X, Y);
             mxy.remove(X * Y);
             mx.remove(X);
             my.remove(Y);
-            vx.remove(X);
-            vy.remove(Y);
-            double t = X + Y;
-            cnt -= (t == t) ? 1 : 0;
+            vx.remove(s, X);
+            vy.remove(s, Y);
+            double t0 = X + Y;
+            cnt -= (t0 == t0) ? 1 : 0;
         }
-        xy(s, s.p, X, Y);
+        xy(s, 0, X, Y);
         mxy.add(X * Y);
         mx.add(X);
         my.add(Y);
-        vx.add(X);
-        vy.add(Y);
+        vx.add(s, X);
+        vy.add(s, Y);
         double t = X + Y;
         cnt += (t == t) ? 1 : 0;
         double c = (double)cnt;
-        double num = (mxy.result(W) - mx.result(W) * my.result(W)) * (c / (c - 1));
-        double den = __builtin_sqrt(vx.result(W) * vy.result(W));
+        const double cf = cnt >= 1 ? s.div(c, cnt - 1) : -c;      // c / (c - 1)
+        double num = (mxy.result(s, W) - mx.result(s, W) * my.result(s, W)) * cf;
+        double den = __builtin_sqrt(vx.result(s, W) * vy.result(s, W));
         s.put(94 + (W == 15 ? 1 : 0), num / den);
-        if (WITH_VC) s.put(93, s.volchg(s.p));
+        if (WITH_VC) s.put(93, s.volchg(0));
     }
 };
 
@@ -457,91 +503,148 @@ template <class... J>
 struct Pack;
 template <>
 struct Pack<> {
+    static constexpr bool kRet = false;
     __device__ void init() {}
     __device__ void step(Step&) {}
 };
+template <class T>
+struct NeedsRet { static constexpr bool value = false; };
+template <int W, bool V>
+struct NeedsRet<Corr<W, V>> { static constexpr bool value = true; };
+template <>
+struct NeedsRet<RetSd3> { static constexpr bool value = true; };
+template <>
+struct NeedsRet<RetSd5x15> { static constexpr bool value = true; };
 template <class H, class... R>
 struct Pack<H, R...> {
+    static constexpr bool kRet = NeedsRet<H>::value || Pack<R...>::kRet;
     H h;
     Pack<R...> r;
     __device__ void init() { h.init(); r.init(); }
     __device__ void step(Step& s) { h.step(s); r.step(s); }
 };
 
-// Static job partition over the 16 waves (roughly equal fp64 work per wave).
+#if AFM_FP_TYPES == 1
+// Static job partition over the 15 job waves of one workgroup (LPT on the per-job VALU count of
+// the compiled step: Corr ~550, RetSd5x15 ~360, VolSd5x15 ~290, BB ~220, VWMA ~170, RetSd3 /
+// VolSd3 / PvtObvPsy ~155, RSI ~115, SMA / MomAccelRocr ~100, MACD ~75, EMA ~60; ~620 per wave),
+// then waves placed so the four SIMDs (waves w, w+4, w+8, w+12; the loader shares SIMD 3) carry
+// equal totals.
+using W0 = Pack<Bbands<14>, Vwma<30>, MomAccelRocr<32>, Sma<42>, Ema<50>>;
+using W1 = Pack<Bbands<44>, Vwma<50>, Sma<6>, Sma<38>, Ema<46>>;
+using W2 = Pack<Bbands<50>, RetSd3, MomAccelRocr<26>, Sma<34>, Ema<42>>;
+using W3 = Pack<Bbands<56>, VolSd3, MomAccelRocr<20>, Sma<30>, Ema<38>>;
+using W4 = Pack<Vwma<6>, Vwma<18>, Rsi<8>, Sma<18>, Ema<18>>;
+using W5 = Pack<RetSd5x15, MomAccelRocr<14>, Sma<14>, Ema<14>>;
+using W6 = Pack<Bbands<38>, Vwma<46>, MomAccelRocr<56>, Macd<24>, Ema<34>>;
+using W7 = Pack<Bbands<32>, Vwma<42>, MomAccelRocr<50>, Macd<18>, Ema<30>>;
+using W8 = Pack<VolSd5x15, PvtObvPsy, Sma<10>, Ema<6>>;
+using W9 = Pack<Corr<5, true>, Ema<10>>;
+using W10 = Pack<Vwma<14>, Vwma<26>, Rsi<20>, Sma<26>, Ema<26>>;
+using W11 = Pack<Vwma<10>, Vwma<22>, Rsi<14>, Sma<22>, Ema<22>>;
+using W12 = Pack<Corr<15, false>, Macd<30>>;
+using W13 = Pack<Bbands<20>, Vwma<34>, MomAccelRocr<38>, Sma<46>>;
+using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>>;
+#else
+// Static job partition: 3 workgroup types x 5 job waves, each wave ~equal fp64 instruction
+// count and <= 168 VGPRs (3 waves / SIMD).
+// type 0: Corr5 (+vol_change), VWMA x12
 using W0 = Pack<Corr<5, true>>;
-using W1 = Pack<Corr<15, false>>;
-using W2 = Pack<Vwma<6>, Vwma<10>, Vwma<14>>;
-using W3 = Pack<Vwma<18>, Vwma<22>, Vwma<26>>;
-using W4 = Pack<Vwma<30>, Vwma<34>, Vwma<38>>;
-using W5 = Pack<Vwma<42>, Vwma<46>, Vwma<50>>;
-using W6 = Pack<Bbands<14>, Bbands<20>, MomAccelRocr<14>, MomAccelRocr<20>>;
-using W7 = Pack<Bbands<26>, Bbands<32>, MomAccelRocr<26>, MomAccelRocr<32>>;
-using W8 = Pack<Bbands<38>, Bbands<44>, MomAccelRocr<38>, MomAccelRocr<44>>;
-using W9 = Pack<Bbands<50>, Bbands<56>, MomAccelRocr<50>, MomAccelRocr<56>>;
-using W10 = Pack<Sma<6>, Sma<10>, Sma<14>, Sma<18>, Sma<22>, Sma<26>>;
-using W11 = Pack<Sma<30>, Sma<34>, Sma<38>, Sma<42>, Sma<46>, Sma<50>>;
-using W12 = Pack<RetSd3, RetSd5x15, PvtObvPsy>;
-using W13 = Pack<VolSd3, VolSd5x15, Rsi<8>>;
-using W14 = Pack<Ema<6>, Ema<10>, Ema<14>, Ema<18>, Ema<22>, Ema<26>, Ema<30>, Ema<34>,
-                 Ema<38>, Ema<42>, Ema<46>, Ema<50>>;
-using W15 = Pack<Macd<18>, Macd<24>, Macd<30>, Rsi<14>, Rsi<20>>;
+using W1 = Pack<Vwma<6>, Vwma<10>, Vwma<14>>;
+using W2 = Pack<Vwma<18>, Vwma<22>, Vwma<26>>;
+using W3 = Pack<Vwma<30>, Vwma<34>, Vwma<38>>;
+using W4 = Pack<Vwma<42>, Vwma<46>, Vwma<50>>;
+// type 1: Corr15, return / volume volatility, PVT/OBV/PSY, RSI, EMAs, MACD, fast SMAs
+using W5 = Pack<Corr<15, false>>;
+using W6 = Pack<RetSd3, RetSd5x15, Macd<18>, Ema<6>, Ema<10>>;
+using W7 = Pack<VolSd3, VolSd5x15, PvtObvPsy, Macd<24>, Ema<14>>;
+using W8 = Pack<Rsi<8>, Rsi<14>, Rsi<20>, Ema<22>, Ema<26>, Ema<30>, Ema<34>, Ema<38>, Ema<42>,
+                  Ema<46>, Ema<50>>;
+using W9 = Pack<Sma<6>, Sma<10>, Sma<14>, Sma<18>, Sma<22>, Sma<26>>;
+// type 2 (close only): Bollinger bands + momentum, slow SMAs, MACD
+using W10 = Pack<Bbands<14>, Bbands<20>, MomAccelRocr<14>, MomAccelRocr<20>>;
+using W11 = Pack<Bbands<26>, Bbands<32>, MomAccelRocr<26>, MomAccelRocr<32>>;
+using W12 = Pack<Bbands<38>, Bbands<44>, MomAccelRocr<38>, MomAccelRocr<44>>;
+using W13 = Pack<Bbands<50>, Bbands<56>, MomAccelRocr<50>, MomAccelRocr<56>>;
+using W14 = Pack<Sma<30>, Sma<34>, Sma<38>, Sma<42>, Sma<46>, Sma<50>, Macd<30>, Ema<18>>;
+
+#endif
+
+// The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
+// job waves (one per chunk + two at each 64-day word end).
+__device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane, int64_t block) {
+    LDS Smem& sm = *smp;
+    const int64_t asset = block * kLanes + lane;
+    const int nch = (int)((a.T + kChunk - 1) / kChunk);
+    double pc[kChunk], pv[kChunk];
+    u64 vb = a.vbits[asset];
+    int pmod = 0;                                   // observations before the staged chunk, mod kRing
+    auto load = [&](int ch) {
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            const int64_t t = (int64_t)ch * kChunk + j;
+            const bool in = t < a.T;
+            pc[j] = in ? a.close[t * a.lda + asset] : 0.0;
+            pv[j] = in ? a.volume[t * a.lda + asset] : 0.0;
+        }
+    };
+    auto stage = [&](int ch) {                      // registers (chunk ch) -> ring + cbyte
+        const int sh = (ch * kChunk) & 63;
+        if (sh == 0 && ch > 0) vb = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
+        const u64 cb = (vb >> sh) & 0xffull;
+        int q = pmod;
+#pragma unroll
+        for (int j = 0; j < kChunk; ++j) {
+            if ((cb >> j) & 1ull) {
+                sm.c[q][lane] = pc[j];
+                sm.v[q][lane] = pv[j];
+                q = q + 1 == kRing ? 0 : q + 1;
+            }
+        }
+        pmod = q;
+        sm.cbyte[ch & 1][lane] = (int)cb;
+    };
+    load(0);
+    stage(0);
+    if (nch > 1) load(1);
+    lds_barrier();                                  // chunk 0 staged
+    for (int ch = 0; ch < nch; ++ch) {
+        if (ch + 1 < nch) {
+            stage(ch + 1);
+            if (ch + 2 < nch) load(ch + 2);
+        }
+        const int sh = (ch * kChunk) & 63;
+        if (sh + kChunk == 64 || ch + 1 == nch) { lds_barrier(); lds_barrier(); }
+        lds_barrier();
+    }
+}
 
 template <class P>
-__device__ __noinline__ void run_wave(const Args a, LDS Smem* smp, int wave, int lane) {
+__device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type, int wave, int lane,
+                                      int64_t block) {
     LDS Smem& sm = *smp;
-    const int64_t asset = (int64_t)blockIdx.x * kLanes + lane;
+    const int64_t asset = block * kLanes + lane;
     const int nch = (int)((a.T + kChunk - 1) / kChunk);
+    const int64_t nwords = (a.T + 63) / 64;
     P jobs;
     jobs.init();
-    int pos = 0;  // observations of this lane before the current chunk
-
-    // prefetch chunk 0 (this wave's 4 days) and its presence word
-    double pc[kLoadSteps], pv[kLoadSteps];
-    u64 vb_next = a.vbits[asset];
-#pragma unroll
-    for (int j = 0; j < kLoadSteps; ++j) {
-        int64_t t = wave * kLoadSteps + j;
-        bool in = t < a.T;
-        pc[j] = in ? a.close[t * a.lda + asset] : 0.0;
-        pv[j] = in ? a.volume[t * a.lda + asset] : 0.0;
-    }
+    int pos = 0, pmod = 0;      // observations of this lane before the current chunk (and mod kRing)
+    u64 nb = 0ull, fb = 0ull;   // this wave's NaN / non-finite bits of the current 64-day word
+    lds_barrier();              // chunk 0 staged
+#ifdef AFM_FP_PROFILE
+    const long long tstart = __builtin_readcyclecounter();
+    const long long treal = (long long)__builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+    long long twait = 0;
+#endif
 
     for (int ch = 0; ch < nch; ++ch) {
-        const u64 vb = vb_next;
-        // ring fill for this chunk (positions pos + rank of the day within the word)
-#pragma unroll
-        for (int j = 0; j < kLoadSteps; ++j) {
-            const int s = wave * kLoadSteps + j;
-            if ((vb >> s) & 1ull) {
-                int q = pos + __popcll(vb & ((1ull << s) - 1ull));
-                sm.c[q & (kRing - 1)][lane] = pc[j];
-                sm.v[q & (kRing - 1)][lane] = pv[j];
-            }
-        }
-        if (wave == 0) {
-            sm.nanmask[lane] = 0ull;
-            sm.badmask[lane] = 0ull;
-        }
-        // prefetch the next chunk while this one is scanned
-        if (ch + 1 < nch) {
-            vb_next = a.vbits[(int64_t)(ch + 1) * a.lda + asset];
-#pragma unroll
-            for (int j = 0; j < kLoadSteps; ++j) {
-                int64_t t = (int64_t)(ch + 1) * kChunk + wave * kLoadSteps + j;
-                bool in = t < a.T;
-                pc[j] = in ? a.close[t * a.lda + asset] : 0.0;
-                pv[j] = in ? a.volume[t * a.lda + asset] : 0.0;
-            }
-        }
-        lds_barrier();
-
+        const int sh = (ch * kChunk) & 63;                 // chunk offset inside its word
+        const u64 cb = (u64)(unsigned)sm.cbyte[ch & 1][lane];
         const int64_t t0 = (int64_t)ch * kChunk;
-        const int steps = (int)min((int64_t)kChunk, a.T - t0);
-        u64 nb = 0ull, fb = 0ull;
-        int p = pos;
-        for (int s = 0; s < steps; ++s) {
-            if ((vb >> s) & 1ull) {
+        int p = pos, pm = pmod;
+#pragma unroll 1
+        for (int s = 0; s < kChunk; ++s) {
+            if ((cb >> s) & 1ull) {
                 Step st;
                 st.sm = smp;
                 st.out = a.out;
@@ -549,48 +652,103 @@ __device__ __noinline__ void run_wave(const Args a, LDS Smem* smp, int wave, int
                 st.cell = (t0 + s) * a.lda + asset;
                 st.lane = lane;
                 st.p = p;
+                st.pm = pm;
                 st.anynan = false;
                 st.anybad = false;
+                if (P::kRet) {
+                    const double r = st.C(0) / st.C(1) - 1;
+                    st.r0 = p >= 1 ? r : qnan();
+                }
                 jobs.step(st);
-                if (st.anynan) nb |= 1ull << s;
-                if (st.anybad) fb |= 1ull << s;
+                if (st.anynan) nb |= 1ull << (sh + s);
+                if (st.anybad) fb |= 1ull << (sh + s);
                 ++p;
+                pm = pm + 1 == kRing ? 0 : pm + 1;
             }
         }
-        if (nb) __atomic_fetch_or(&sm.nanmask[lane], nb, __ATOMIC_RELAXED);
-        if (fb) __atomic_fetch_or(&sm.badmask[lane], fb, __ATOMIC_RELAXED);
-        lds_barrier();
-        if (wave == 0) {
-            a.nanfree[(int64_t)ch * a.lda + asset] = vb & ~sm.nanmask[lane];
-            if (a.finite) a.finite[(int64_t)ch * a.lda + asset] = vb & ~sm.badmask[lane];
-        }
         pos = p;
+        pmod = pm;
+        if (sh + kChunk == 64 || ch + 1 == nch) {          // word end: uniform in the workgroup
+            if (wave == 0) { sm.nanmask[lane] = nb; sm.badmask[lane] = fb; }
+            lds_barrier();
+            if (wave != 0) {
+                if (nb) __atomic_fetch_or(&sm.nanmask[lane], nb, __ATOMIC_RELAXED);
+                if (fb) __atomic_fetch_or(&sm.badmask[lane], fb, __ATOMIC_RELAXED);
+            }
+            lds_barrier();
+            if (wave == 0) {
+                const int64_t o = ((int64_t)type * nwords + ((int64_t)(ch * kChunk) >> 6)) * a.lda
+                                  + asset;
+                a.nanpart[o] = sm.nanmask[lane];
+                a.badpart[o] = sm.badmask[lane];
+            }
+            nb = 0ull;
+            fb = 0ull;
+        }
+#ifdef AFM_FP_PROFILE
+        const long long tb = __builtin_readcyclecounter();
+        lds_barrier();
+        twait += __builtin_readcyclecounter() - tb;
+#else
+        lds_barrier();
+#endif
     }
+#ifdef AFM_FP_PROFILE
+    if (lane == 0) {
+        const long long tot = __builtin_readcyclecounter() - tstart;
+        g_wave_cycles[(blockIdx.x * kJobWaves + wave) * 3 % (1 << 16)] = tot;
+        g_wave_cycles[((blockIdx.x * kJobWaves + wave) * 3 + 1) % (1 << 16)] = twait;
+        g_wave_cycles[((blockIdx.x * kJobWaves + wave) * 3 + 2) % (1 << 16)] = treal;
+    }
+#endif
 }
 
-__global__ __launch_bounds__(kLanes * kWaves) void factor_panel_kernel(Args a) {
+__global__ __launch_bounds__(kLanes * kWaves, kMinWavesPerSimd) void factor_panel_kernel(Args a) {
     __shared__ Smem sm_;
     LDS Smem* sm = (LDS Smem*)&sm_;
     const int lane = threadIdx.x & (kLanes - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    switch (wave) {
-        case 0: run_wave<W0>(a, sm, wave, lane); break;
-        case 1: run_wave<W1>(a, sm, wave, lane); break;
-        case 2: run_wave<W2>(a, sm, wave, lane); break;
-        case 3: run_wave<W3>(a, sm, wave, lane); break;
-        case 4: run_wave<W4>(a, sm, wave, lane); break;
-        case 5: run_wave<W5>(a, sm, wave, lane); break;
-        case 6: run_wave<W6>(a, sm, wave, lane); break;
-        case 7: run_wave<W7>(a, sm, wave, lane); break;
-        case 8: run_wave<W8>(a, sm, wave, lane); break;
-        case 9: run_wave<W9>(a, sm, wave, lane); break;
-        case 10: run_wave<W10>(a, sm, wave, lane); break;
-        case 11: run_wave<W11>(a, sm, wave, lane); break;
-        case 12: run_wave<W12>(a, sm, wave, lane); break;
-        case 13: run_wave<W13>(a, sm, wave, lane); break;
-        case 14: run_wave<W14>(a, sm, wave, lane); break;
-        default: run_wave<W15>(a, sm, wave, lane); break;
+    const int type = (int)(blockIdx.x % kTypes);
+    const int64_t block = blockIdx.x / kTypes;
+    if (threadIdx.x < 128) sm->rtab[threadIdx.x] = 1.0 / (double)threadIdx.x;
+    // (the loader's first barrier also publishes rtab)
+    if (wave == kJobWaves) { load_wave(a, sm, lane, block); return; }
+    switch (type * kJobWaves + wave) {
+        case 0: run_wave<W0>(a, sm, type, wave, lane, block); break;
+        case 1: run_wave<W1>(a, sm, type, wave, lane, block); break;
+        case 2: run_wave<W2>(a, sm, type, wave, lane, block); break;
+        case 3: run_wave<W3>(a, sm, type, wave, lane, block); break;
+        case 4: run_wave<W4>(a, sm, type, wave, lane, block); break;
+        case 5: run_wave<W5>(a, sm, type, wave, lane, block); break;
+        case 6: run_wave<W6>(a, sm, type, wave, lane, block); break;
+        case 7: run_wave<W7>(a, sm, type, wave, lane, block); break;
+        case 8: run_wave<W8>(a, sm, type, wave, lane, block); break;
+        case 9: run_wave<W9>(a, sm, type, wave, lane, block); break;
+        case 10: run_wave<W10>(a, sm, type, wave, lane, block); break;
+        case 11: run_wave<W11>(a, sm, type, wave, lane, block); break;
+        case 12: run_wave<W12>(a, sm, type, wave, lane, block); break;
+        case 13: run_wave<W13>(a, sm, type, wave, lane, block); break;
+        default: run_wave<W14>(a, sm, type, wave, lane, block); break;
     }
+}
+
+// nanfree = present & no type flagged a NaN; finite = present & no type flagged a non-finite
+__global__ __launch_bounds__(256) void masks_kernel(int64_t nwords, int64_t lda,
+                                                    const uint64_t* vbits, const uint64_t* nanpart,
+                                                    const uint64_t* badpart, uint64_t* nanfree,
+                                                    uint64_t* finite) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = nwords * lda;
+    if (i >= n) return;
+    u64 nm = 0ull, bm = 0ull;
+#pragma unroll
+    for (int t = 0; t < kTypes; ++t) {
+        nm |= nanpart[t * n + i];
+        bm |= badpart[t * n + i];
+    }
+    const u64 v = vbits[i];
+    nanfree[i] = v & ~nm;
+    if (finite) finite[i] = v & ~bm;
 }
 
 // target = excess_ret1d.shift(-1), tmr_ret1d = ret1d.shift(-1) (No-talib.py:90-91): the value of
@@ -630,6 +788,13 @@ __global__ __launch_bounds__(256) void labels_kernel(int64_t T, int64_t lda, con
 }  // namespace
 }  // namespace afm
 
+#ifdef AFM_FP_PROFILE
+extern "C" int afm_debug_wave_cycles(long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(afm::g_wave_cycles), sizeof(long long) * n) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                                const double* close, const double* volume, const double* ret1d,
                                const double* excess, const uint64_t* valid_bits, double* out,
@@ -640,6 +805,10 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     AFM_CHECK_ARG(close && volume && ret1d && excess && valid_bits && out && nanfree_bits,
                   "null buffer");
     AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
+    const int64_t nwords = (T + 63) / 64;
+    uint64_t* part = nullptr;
+    AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * afm::kTypes * nwords * lda,
+                           ctx->stream));
     afm::Args a;
     a.T = T;
     a.lda = lda;
@@ -648,14 +817,23 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     a.volume = (const GLB double*)volume;
     a.vbits = (const GLB uint64_t*)valid_bits;
     a.out = (GLB double*)out;
-    a.nanfree = (GLB uint64_t*)nanfree_bits;
-    a.finite = (GLB uint64_t*)finite_bits;
-    dim3 grid((unsigned)(lda / 64));
-    hipLaunchKernelGGL(afm::factor_panel_kernel, grid, dim3(64 * 16), 0, ctx->stream, a);
+    a.nanpart = (GLB uint64_t*)part;
+    a.badpart = (GLB uint64_t*)(part + afm::kTypes * nwords * lda);
+    const int64_t nblk = (A + 63) / 64;
+    hipLaunchKernelGGL(afm::factor_panel_kernel, dim3((unsigned)(nblk * afm::kTypes)),
+                       dim3(64 * afm::kWaves), 0, ctx->stream, a);  // kJobWaves + loader
+    AFM_HIP(hipGetLastError());
+    const int64_t nw = nwords * lda;
+    // columns past A (lda padding) carry no presence: their mask words come from valid_bits
+    // (zero there), and the factor kernel never ran on blocks past ceil(A/64)
+    hipLaunchKernelGGL(afm::masks_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0,
+                       ctx->stream, nwords, lda, valid_bits, part, part + afm::kTypes * nw,
+                       nanfree_bits, finite_bits);
     AFM_HIP(hipGetLastError());
     dim3 g2((unsigned)(lda / 64), (unsigned)((T + 3) / 4));
     hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, lda, excess, ret1d,
                        valid_bits, out + 96 * a.plane, out + 97 * a.plane);
     AFM_HIP(hipGetLastError());
+    AFM_HIP(hipFreeAsync(part, ctx->stream));
     return AFM_OK;
 }

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Time individual pipeline stages on the config-C panel (profiling / iteration helper).
+Usage: python tools/stage_bench.py [--stages factors,xs_gram] [--reps N] [--assets A --days T]"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "alpha-multi-factor-models_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--stages", default="all")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--assets", type=int, default=10000)
+    ap.add_argument("--days", type=int, default=5040)
+    args = ap.parse_args()
+    import torch
+    import afm
+    from afm.pipeline import STAGES, Pipeline
+    from afm.synthetic import make_panel
+    torch.cuda.set_device(0)
+    grid = afm.PanelGrid.from_panel(make_panel(args.assets, args.days, seed=2023))
+    pipe = Pipeline(grid)
+    pipe.step()
+    torch.cuda.synchronize()
+    want = STAGES if args.stages == "all" else args.stages.split(",")
+    for _ in range(args.reps):
+        ev = {st: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for st in STAGES}
+        pipe.step(ev, only=set(want))
+        torch.cuda.synchronize()
+        print(" ".join(f"{st}={ev[st][0].elapsed_time(ev[st][1]):.3f}" for st in want), flush=True)
+
+
+if __name__ == "__main__":
+    main()
