@@ -754,12 +754,13 @@ __global__ __launch_bounds__(256) void masks_kernel(int64_t nwords, int64_t lda,
 // target = excess_ret1d.shift(-1), tmr_ret1d = ret1d.shift(-1) (No-talib.py:90-91): the value of
 // the asset's NEXT present day, NaN on its last one.  One thread per cell, next present day found
 // from the presence words (ctz), rows read/written coalesced.
-__global__ __launch_bounds__(256) void labels_kernel(int64_t T, int64_t lda, const double* excess,
+__global__ __launch_bounds__(256) void labels_kernel(int64_t T, int64_t t_begin, int64_t t_end,
+                                                     int64_t lda, const double* excess,
                                                      const double* ret1d, const uint64_t* vbits,
                                                      double* target, double* tmr) {
     const int64_t a = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-    const int64_t t = (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (t >= T) return;
+    const int64_t t = t_begin + (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (t >= t_end) return;
     const int64_t nch = (T + 63) / 64;
     int64_t ch = t >> 6;
     const int s = (int)(t & 63);
@@ -831,9 +832,25 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                        nanfree_bits, finite_bits);
     AFM_HIP(hipGetLastError());
     dim3 g2((unsigned)(lda / 64), (unsigned)((T + 3) / 4));
-    hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, lda, excess, ret1d,
-                       valid_bits, out + 96 * a.plane, out + 97 * a.plane);
+    hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, (int64_t)0, T, lda,
+                       excess, ret1d, valid_bits, out + 96 * a.plane, out + 97 * a.plane);
     AFM_HIP(hipGetLastError());
     AFM_HIP(hipFreeAsync(part, ctx->stream));
+    return AFM_OK;
+}
+
+extern "C" int afm_labels_f64(afm_ctx* ctx, int64_t T, int64_t lda, int64_t t0, int64_t t1,
+                              const double* excess, const double* ret1d,
+                              const uint64_t* valid_bits, double* target, double* tmr) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && lda > 0 && lda % 64 == 0, "bad panel shape");
+    AFM_CHECK_ARG(excess && ret1d && valid_bits && target && tmr, "null buffer");
+    t0 = t0 < 0 ? 0 : t0;
+    t1 = t1 > T ? T : t1;
+    if (t1 <= t0) return AFM_OK;
+    dim3 g2((unsigned)(lda / 64), (unsigned)((t1 - t0 + 3) / 4));
+    hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, t0, t1, lda, excess,
+                       ret1d, valid_bits, target, tmr);
+    AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

@@ -621,6 +621,24 @@ extern "C" int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const doub
     return AFM_OK;
 }
 
+extern "C" int afm_pool_segments_f64(afm_ctx* ctx, const double* gram, const double* shift,
+                                     int p, int64_t nseg, int64_t per, double* out_gram,
+                                     double* out_shift) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(p >= 1 && p + 2 <= kMaxF, "need 1 <= p <= 110");
+    AFM_CHECK_ARG(gram && shift && out_gram && out_shift && nseg >= 0 && per >= 1, "bad arguments");
+    if (nseg == 0) return AFM_OK;
+    const int p2 = p + 2;
+    const size_t lds = sizeof(double) * p2 * p2;
+    AFM_HIP(hipFuncSetAttribute((const void*)pool_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int64_t nb = (nseg + per - 1) / per;
+    hipLaunchKernelGGL(pool_kernel, dim3((unsigned)nb), dim3(kThreads), lds, ctx->stream, gram,
+                       shift, p2, nseg, per, out_gram, out_shift);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
 extern "C" int afm_predict_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
                                int64_t t0, int64_t nt, const int32_t* cols, int p,
                                const double* beta, int64_t beta_stride, const uint64_t* bits,

@@ -108,28 +108,21 @@ def main():
 
     t0 = time.perf_counter()
     p = make_panel(args.assets, args.days, seed=args.seed)
-    if world > 1:
-        # interim multi-GPU mode: each rank runs the full pipeline on its slice of assets
-        from afm.synthetic import Panel, round_up
-        lo = (args.assets * rank) // world
-        hi = (args.assets * (rank + 1)) // world
-        lda = round_up(hi - lo)
-
-        def sl(x, fill):
-            o = np.full((p.T, lda), fill, dtype=x.dtype)
-            o[:, : hi - lo] = x[:, lo:hi]
-            return o
-        p = Panel(dates=p.dates, ids=p.ids[lo:hi], close=sl(p.close, np.nan),
-                  volume=sl(p.volume, np.nan), ret1d=sl(p.ret1d, np.nan),
-                  excess=sl(p.excess, np.nan), valid=sl(p.valid, False),
-                  tradable=sl(p.tradable, False), group_id=p.group_id[lo:hi])
     grid = afm.PanelGrid.from_panel(p, device=dev)
     del p
-    n_ad = grid.n_asset_days()
-    pipe = Pipeline(grid)
+    n_ad = grid.n_asset_days()                         # the whole panel (strong scaling)
+    if world > 1:
+        from afm.sharded import EXCHANGE_STAGES, Comm, ShardedPipeline
+        pipe = ShardedPipeline(grid, Comm())
+        stages = EXCHANGE_STAGES
+        n_ad_local = pipe.n_asset_days_local()
+    else:
+        pipe = Pipeline(grid)
+        stages = STAGES
+        n_ad_local = n_ad
     torch.cuda.synchronize()
-    log(f"[rank {rank}] panel {grid.A}x{grid.T} ({n_ad} asset-days) ready in "
-        f"{time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] panel {grid.A}x{grid.T} ({n_ad} asset-days, {n_ad_local} in this rank's "
+        f"factor shard) ready in {time.perf_counter() - t0:.1f}s")
 
     for _ in range(args.warmup):
         pipe.step()
@@ -140,7 +133,7 @@ def main():
             f"per-date ranks {np.bincount(s['ranks'])[-3:]}, qp status {np.bincount(s['status'])}")
 
     evs = [{st: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for st in STAGES} for _ in range(args.steps)]
+            for st in stages} for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -152,24 +145,20 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stage_ms = {st: sum(e[st][0].elapsed_time(e[st][1]) for e in evs) / args.steps
-                for st in STAGES}
+                for st in stages}
 
     total_ad = n_ad
     if world > 1:
-        t = torch.tensor([elapsed, float(n_ad)], dtype=torch.float64, device=dev)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0])
-        total_ad = int(sm[1])
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         # roofline of the dominant kernel: factor panel (HBM) or the per-date Gram (fp64 MFMA)
         p = pipe.p
-        fac_gbs = FACTOR_BYTES_PER_AD * n_ad / (stage_ms["factors"] * 1e-3) / 1e9
-        gram_rows = float(pipe.nobs.sum().item())
+        fac_gbs = FACTOR_BYTES_PER_AD * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
+        gram_rows = float(pipe.nobs.sum().item()) / world      # this rank's share of the rows
         gram_tfs = gram_rows * (p + 2) * (p + 3) / (stage_ms["xs_gram"] * 1e-3) / 1e12
         if stage_ms["factors"] >= stage_ms["xs_gram"]:
             roof = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS,
@@ -194,7 +183,9 @@ def main():
                                    f"factors -> per-date OLS on 96 factors + FM -> pooled OLS -> "
                                    f"predict -> rolling-252 cov + exact KKT top/bottom-10 -> PnL",
                        "assets": args.assets, "days": args.days, "asset_days": total_ad,
-                       "parallelism": f"asset-shard x{world}" if world > 1 else "single"},
+                       "parallelism": (f"asset shards (factors, partial Grams) + date shards "
+                                       f"(solves, rebalance) x{world}") if world > 1
+                       else "single"},
             "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
             "roofline": roof,
             "secondary": {"factor_panel_GBps": round(fac_gbs, 1),

@@ -59,6 +59,14 @@ int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                     const double* excess, const uint64_t* valid_bits,
                     double* out, uint64_t* nanfree_bits, uint64_t* finite_bits);
 
+/* target = excess_ret1d.shift(-1), tmr_ret1d = ret1d.shift(-1) per asset (No-talib.py:90-91) for
+ * the grid dates [t0, t1) only (the label planes of afm_factors_f64 for a sub-range; used where
+ * the factor panel itself is sharded by asset but the history/PnL planes are needed for every
+ * asset).  Absent cells are not written. */
+int afm_labels_f64(afm_ctx* ctx, int64_t T, int64_t lda, int64_t t0, int64_t t1,
+                   const double* excess, const double* ret1d, const uint64_t* valid_bits,
+                   double* target, double* tmr);
+
 /* ---- R1: cross-sectional regression ---------------------------------------------------------
  * Segmented shifted Gram on fp64 MFMA.  Segment t (t = seg0 .. seg0+nseg-1) is the rows
  * [t*seg_stride, t*seg_stride + seg_rows) of every column; column c starts at base + c*col_stride.
@@ -79,6 +87,11 @@ int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double* shift, int
  * of KKT:582-583 over the union of the segments' rows. */
 int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
                          int64_t nseg, double* out_gram, double* out_shift);
+/* Segmented version: out[b] combines segments [b*per, min((b+1)*per, nseg)) in order (Chan), for
+ * b < ceil(nseg/per) -- e.g. the per-rank partial moments of one date (multi-GPU asset shards), or
+ * the 64-date blocks of afm_pool_moments_f64's first pass.  Segments with n = 0 are skipped. */
+int afm_pool_segments_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
+                          int64_t nseg, int64_t per, double* out_gram, double* out_shift);
 /* pred[t][a] = beta[t-t0][0] + sum_j beta[t-t0][1+j] * x_cols[j][t][a] on grid rows with a mask
  * bit (NaN elsewhere), t in [t0, t0+nt); beta_stride = 0 applies one coefficient vector.
  * ycheck >= 0: additionally require column ycheck finite (e.g. the label of a dropna'd row). */
