@@ -11,10 +11,10 @@
 //  * One workgroup = one 64-asset block: 15 job waves (balanced by the VALU count of each job's
 //    compiled step, and so that the four SIMDs carry equal totals) + 1 loader wave; the kernel
 //    is VALU-issue-bound (~86% of each SIMD's cycles).  An LDS ring holds the last kRing
-//    present observations of close and volume per lane.  (AFM_FP_TYPES=3 splits a block's jobs
-//    over 3 workgroups; measured on MI355X, workgroups of 78 KB LDS do not co-reside -- the
-//    two-per-CU limit was between 52 and 56 KB -- so that layout runs in two rounds and is
-//    slower at 10k assets; kept for few-block shards.)
+//    present observations of close and volume per lane.  A shard with few blocks (multi-GPU)
+//    splits each block's 15 job waves over 3, 5 or 15 workgroups instead, so that ~all CUs work
+//    (each split needs its own ring; measured on MI355X, workgroups of 78 KB LDS do not
+//    co-reside -- the two-per-CU limit was between 52 and 56 KB -- hence one per CU).
 //  * The loader wave is the only one that reads global memory: it fills the ring one chunk
 //    ahead of the scan and publishes each chunk's presence bits.  The job waves only store, so
 //    they never wait on vmcnt (loads and stores share the counter on gfx950: a wave that both
@@ -36,6 +36,8 @@
 // Algorithmic traffic per present asset-day: 32 B of inputs read + 98 x 8 B written = 816 B.
 #include "afm_internal.h"
 
+#include <cstdlib>
+
 #pragma clang fp contract(off)
 
 namespace afm {
@@ -50,13 +52,7 @@ constexpr int kRing = AFM_FP_RING;     // experiments only
 #else
 constexpr int kRing = 57 + 2 * kChunk + 1;
 #endif
-#ifndef AFM_FP_TYPES
-#define AFM_FP_TYPES 1
-#endif
-constexpr int kTypes = AFM_FP_TYPES;        // workgroups (job-set types) per 64-asset block
-constexpr int kJobWaves = 15 / kTypes;      // job waves per workgroup
-constexpr int kWaves = kJobWaves + 1;       // + one loader wave (the last)
-constexpr int kMinWavesPerSimd = kTypes == 1 ? 4 : 3;
+constexpr int kJobSets = 15;      // job waves per 64-asset block (W0..W14 below)
 
 typedef unsigned long long u64;
 #ifdef AFM_FP_PROFILE
@@ -105,8 +101,9 @@ struct Args {
     const GLB double* volume;
     const GLB uint64_t* vbits;
     GLB double* out;
-    GLB uint64_t* nanpart;     // [kTypes][nch][lda] per-type "some output NaN" bits
-    GLB uint64_t* badpart;     // [kTypes][nch][lda] per-type "some output non-finite" bits
+    GLB uint64_t* nanpart;     // [types][nch][lda] per-workgroup-type "some output NaN" bits
+    GLB uint64_t* badpart;     // [types][nch][lda] per-type "some output non-finite" bits
+    int types;                 // workgroups per 64-asset block (1, 3, 5 or 15)
 };
 
 // Per-lane view of one (asset, present day) step.  Lookback L reads observation p - L.
@@ -524,7 +521,6 @@ struct Pack<H, R...> {
     __device__ void step(Step& s) { h.step(s); r.step(s); }
 };
 
-#if AFM_FP_TYPES == 1
 // Static job partition over the 15 job waves of one workgroup (LPT on the per-job VALU count of
 // the compiled step: Corr ~550, RetSd5x15 ~360, VolSd5x15 ~290, BB ~220, VWMA ~170, RetSd3 /
 // VolSd3 / PvtObvPsy ~155, RSI ~115, SMA / MomAccelRocr ~100, MACD ~75, EMA ~60; ~620 per wave),
@@ -545,30 +541,6 @@ using W11 = Pack<Vwma<10>, Vwma<22>, Rsi<14>, Sma<22>, Ema<22>>;
 using W12 = Pack<Corr<15, false>, Macd<30>>;
 using W13 = Pack<Bbands<20>, Vwma<34>, MomAccelRocr<38>, Sma<46>>;
 using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>>;
-#else
-// Static job partition: 3 workgroup types x 5 job waves, each wave ~equal fp64 instruction
-// count and <= 168 VGPRs (3 waves / SIMD).
-// type 0: Corr5 (+vol_change), VWMA x12
-using W0 = Pack<Corr<5, true>>;
-using W1 = Pack<Vwma<6>, Vwma<10>, Vwma<14>>;
-using W2 = Pack<Vwma<18>, Vwma<22>, Vwma<26>>;
-using W3 = Pack<Vwma<30>, Vwma<34>, Vwma<38>>;
-using W4 = Pack<Vwma<42>, Vwma<46>, Vwma<50>>;
-// type 1: Corr15, return / volume volatility, PVT/OBV/PSY, RSI, EMAs, MACD, fast SMAs
-using W5 = Pack<Corr<15, false>>;
-using W6 = Pack<RetSd3, RetSd5x15, Macd<18>, Ema<6>, Ema<10>>;
-using W7 = Pack<VolSd3, VolSd5x15, PvtObvPsy, Macd<24>, Ema<14>>;
-using W8 = Pack<Rsi<8>, Rsi<14>, Rsi<20>, Ema<22>, Ema<26>, Ema<30>, Ema<34>, Ema<38>, Ema<42>,
-                  Ema<46>, Ema<50>>;
-using W9 = Pack<Sma<6>, Sma<10>, Sma<14>, Sma<18>, Sma<22>, Sma<26>>;
-// type 2 (close only): Bollinger bands + momentum, slow SMAs, MACD
-using W10 = Pack<Bbands<14>, Bbands<20>, MomAccelRocr<14>, MomAccelRocr<20>>;
-using W11 = Pack<Bbands<26>, Bbands<32>, MomAccelRocr<26>, MomAccelRocr<32>>;
-using W12 = Pack<Bbands<38>, Bbands<44>, MomAccelRocr<38>, MomAccelRocr<44>>;
-using W13 = Pack<Bbands<50>, Bbands<56>, MomAccelRocr<50>, MomAccelRocr<56>>;
-using W14 = Pack<Sma<30>, Sma<34>, Sma<38>, Sma<42>, Sma<46>, Sma<50>, Macd<30>, Ema<18>>;
-
-#endif
 
 // The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
 // job waves (one per chunk + two at each 64-day word end).
@@ -696,24 +668,32 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
 #ifdef AFM_FP_PROFILE
     if (lane == 0) {
         const long long tot = __builtin_readcyclecounter() - tstart;
-        g_wave_cycles[(blockIdx.x * kJobWaves + wave) * 3 % (1 << 16)] = tot;
-        g_wave_cycles[((blockIdx.x * kJobWaves + wave) * 3 + 1) % (1 << 16)] = twait;
-        g_wave_cycles[((blockIdx.x * kJobWaves + wave) * 3 + 2) % (1 << 16)] = treal;
+        const int jw = kJobSets / a.types;
+        g_wave_cycles[(blockIdx.x * jw + wave) * 3 % (1 << 16)] = tot;
+        g_wave_cycles[((blockIdx.x * jw + wave) * 3 + 1) % (1 << 16)] = twait;
+        g_wave_cycles[((blockIdx.x * jw + wave) * 3 + 2) % (1 << 16)] = treal;
     }
 #endif
 }
 
-__global__ __launch_bounds__(kLanes * kWaves, kMinWavesPerSimd) void factor_panel_kernel(Args a) {
+// TYPES workgroups per block, each with J = 15 / TYPES job waves (job sets W[J*type + wave]) and
+// a loader wave.  TYPES = 1 (15 + 1 waves, 4 waves / SIMD) when the blocks fill the chip; more
+// when a shard has few blocks (multi-GPU): every workgroup needs its own 78-KB ring, so they run
+// one per CU.
+template <int TYPES>
+__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1), TYPES == 1 ? 4 : 2)
+void factor_panel_kernel(Args a) {
+    constexpr int J = kJobSets / TYPES;
     __shared__ Smem sm_;
     LDS Smem* sm = (LDS Smem*)&sm_;
     const int lane = threadIdx.x & (kLanes - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int type = (int)(blockIdx.x % kTypes);
-    const int64_t block = blockIdx.x / kTypes;
+    const int type = (int)(blockIdx.x % TYPES);
+    const int64_t block = blockIdx.x / TYPES;
     if (threadIdx.x < 128) sm->rtab[threadIdx.x] = 1.0 / (double)threadIdx.x;
     // (the loader's first barrier also publishes rtab)
-    if (wave == kJobWaves) { load_wave(a, sm, lane, block); return; }
-    switch (type * kJobWaves + wave) {
+    if (wave == J) { load_wave(a, sm, lane, block); return; }
+    switch (type * J + wave) {
         case 0: run_wave<W0>(a, sm, type, wave, lane, block); break;
         case 1: run_wave<W1>(a, sm, type, wave, lane, block); break;
         case 2: run_wave<W2>(a, sm, type, wave, lane, block); break;
@@ -733,7 +713,7 @@ __global__ __launch_bounds__(kLanes * kWaves, kMinWavesPerSimd) void factor_pane
 }
 
 // nanfree = present & no type flagged a NaN; finite = present & no type flagged a non-finite
-__global__ __launch_bounds__(256) void masks_kernel(int64_t nwords, int64_t lda,
+__global__ __launch_bounds__(256) void masks_kernel(int64_t nwords, int64_t lda, int types,
                                                     const uint64_t* vbits, const uint64_t* nanpart,
                                                     const uint64_t* badpart, uint64_t* nanfree,
                                                     uint64_t* finite) {
@@ -741,8 +721,7 @@ __global__ __launch_bounds__(256) void masks_kernel(int64_t nwords, int64_t lda,
     const int64_t n = nwords * lda;
     if (i >= n) return;
     u64 nm = 0ull, bm = 0ull;
-#pragma unroll
-    for (int t = 0; t < kTypes; ++t) {
+    for (int t = 0; t < types; ++t) {
         nm |= nanpart[t * n + i];
         bm |= badpart[t * n + i];
     }
@@ -807,8 +786,19 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                   "null buffer");
     AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
     const int64_t nwords = (T + 63) / 64;
+    const int64_t nblk = (A + 63) / 64;
+    // workgroups per block: the most job-set splits that still fit one workgroup per CU
+    int ncu = 256;
+    AFM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    int types = 1;
+    for (int t : {3, 5, 15})
+        if (nblk * t <= ncu) types = t;
+    if (const char* e = getenv("AFM_FP_TYPES")) {                 // tuning override
+        const int t = atoi(e);
+        if (t == 1 || t == 3 || t == 5 || t == 15) types = t;
+    }
     uint64_t* part = nullptr;
-    AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * afm::kTypes * nwords * lda,
+    AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * types * nwords * lda,
                            ctx->stream));
     afm::Args a;
     a.T = T;
@@ -819,16 +809,25 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     a.vbits = (const GLB uint64_t*)valid_bits;
     a.out = (GLB double*)out;
     a.nanpart = (GLB uint64_t*)part;
-    a.badpart = (GLB uint64_t*)(part + afm::kTypes * nwords * lda);
-    const int64_t nblk = (A + 63) / 64;
-    hipLaunchKernelGGL(afm::factor_panel_kernel, dim3((unsigned)(nblk * afm::kTypes)),
-                       dim3(64 * afm::kWaves), 0, ctx->stream, a);  // kJobWaves + loader
+    a.badpart = (GLB uint64_t*)(part + types * nwords * lda);
+    a.types = types;
+    const dim3 grid((unsigned)(nblk * types));
+    switch (types) {
+        case 1: hipLaunchKernelGGL(afm::factor_panel_kernel<1>, grid, dim3(64 * 16), 0,
+                                   ctx->stream, a); break;
+        case 3: hipLaunchKernelGGL(afm::factor_panel_kernel<3>, grid, dim3(64 * 6), 0,
+                                   ctx->stream, a); break;
+        case 5: hipLaunchKernelGGL(afm::factor_panel_kernel<5>, grid, dim3(64 * 4), 0,
+                                   ctx->stream, a); break;
+        default: hipLaunchKernelGGL(afm::factor_panel_kernel<15>, grid, dim3(64 * 2), 0,
+                                    ctx->stream, a); break;
+    }
     AFM_HIP(hipGetLastError());
     const int64_t nw = nwords * lda;
     // columns past A (lda padding) carry no presence: their mask words come from valid_bits
     // (zero there), and the factor kernel never ran on blocks past ceil(A/64)
     hipLaunchKernelGGL(afm::masks_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0,
-                       ctx->stream, nwords, lda, valid_bits, part, part + afm::kTypes * nw,
+                       ctx->stream, nwords, lda, types, valid_bits, part, part + types * nw,
                        nanfree_bits, finite_bits);
     AFM_HIP(hipGetLastError());
     dim3 g2((unsigned)(lda / 64), (unsigned)((T + 3) / 4));

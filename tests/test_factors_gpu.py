@@ -57,6 +57,31 @@ def test_factor_grid_vs_oracle(A, T, seed, kw):
     assert np.array_equal(nf, exp)
 
 
+@pytest.mark.parametrize("types", ["1", "3", "5", "15"])
+def test_factor_workgroup_splits_identical(types, monkeypatch):
+    """Every split of a block's 15 job waves over 1, 3, 5 or 15 workgroups (chosen from the
+    shard's block count; AFM_FP_TYPES overrides) gives the same bit-exact panel and masks."""
+    import torch
+    import afm
+    from afm.synthetic import make_panel
+    p = make_panel(200, 500, seed=9, edge_cases=True, hole_frac=0.01, listing_frac=0.2)
+    grid = afm.PanelGrid.from_panel(p)
+    monkeypatch.setenv("AFM_FP_TYPES", types)
+    fin = torch.zeros_like(grid.vbits)
+    out, nanfree = afm.factor_panel(grid, finite=fin)
+    torch.cuda.synchronize()
+    tt, aa, ref = oracle_panel(p)
+    got = out[:, torch.from_numpy(tt).cuda(), torch.from_numpy(aa).cuda()].T.cpu().numpy()
+    assert same(got, ref), mismatch_report(got, ref, afm.FACTOR_NAMES)
+    nf = afm.unpack_bits(nanfree, p.T).cpu().numpy()
+    ff = afm.unpack_bits(fin, p.T).cpu().numpy()
+    exp_n = np.zeros_like(p.valid)
+    exp_n[tt, aa] = ~np.isnan(ref[:, :96]).any(axis=1)
+    exp_f = np.zeros_like(p.valid)
+    exp_f[tt, aa] = np.isfinite(ref[:, :96]).all(axis=1)
+    assert np.array_equal(nf, exp_n) and np.array_equal(ff, exp_f)
+
+
 def test_factor_kernel_rejects_bad_shapes():
     import torch
     import afm
