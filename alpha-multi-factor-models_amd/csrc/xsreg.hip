@@ -298,9 +298,14 @@ __global__ __launch_bounds__(kThreads, MINW) void gram_kernel(GramArgs g) {
 }
 
 // ---- per-segment OLS from the shifted Gram -------------------------------------------------
-// C = G'[1:,1:] - G'[0,1:] G'[0,1:]^T / n (centered moments of [x, y]); scale to unit diagonal,
-// Cholesky with a relative pivot threshold (a pivot below tol drops the regressor: beta = 0),
-// beta = D b, intercept = ybar - xbar . beta.  One workgroup per segment, matrices in LDS.
+// C = G'[1:,1:] - G'[0,1:] G'[0,1:]^T / n: centered moments of the AUGMENTED [x, y] (q = p + 1
+// columns), x scaled to unit diagonal.  A right-looking Cholesky over the p x-columns also
+// eliminates the y row, which leaves z = L^-1 r in it (forward substitution for free); a pivot
+// below tol drops its regressor (beta = 0).  The factor is kept unscaled -- the update is
+// M[i][j] -= M[i][k] M[j][k] / d_k -- so each column costs ONE barrier; back substitution
+// beta_j = (M[y][j] - sum_{i>j} M[i][j] beta_i) / d_j runs in one wave.  beta = D b,
+// intercept = ybar - xbar . beta.  One workgroup per segment, the matrix in LDS (76 KB at
+// p = 96: two workgroups per CU).
 struct SolveArgs {
     const double* gram;      // [nseg][p2][p2]
     const double* shift;     // [nseg][p2]
@@ -314,14 +319,14 @@ struct SolveArgs {
 constexpr int kMaxP = kMaxF - 2;
 
 __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
-    __shared__ double M[kMaxP][kMaxP + 1];
-    __shared__ double rhs[kMaxP];
-    __shared__ double dsc[kMaxP];
+    extern __shared__ __attribute__((aligned(16))) double M[];    // [q][ld], lower triangle used
+    __shared__ double dsc[kMaxP + 1];
+    __shared__ double dk[kMaxP];
     __shared__ double mean[kMaxP + 2];
+    __shared__ double bvec[kMaxP];
     __shared__ int drop[kMaxP];
-    __shared__ double piv;
     const int tid = threadIdx.x;
-    const int p = s.p, p2 = p + 2;
+    const int p = s.p, p2 = p + 2, q = p + 1, ld = q + 1;
     const double* G = s.gram + (int64_t)blockIdx.x * p2 * p2;
     const double* sf = s.shift + (int64_t)blockIdx.x * p2;
     const double n = G[0];
@@ -333,78 +338,63 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
         return;
     }
     for (int j = tid; j < p2; j += kThreads) mean[j] = (j == 0) ? 1.0 : G[j] / n;   // shifted
-    __syncthreads();
-    for (int i = tid; i < p * p; i += kThreads) {
-        int r = i / p, c = i % p;
-        M[r][c] = G[(r + 1) * p2 + (c + 1)] - G[r + 1] * G[c + 1] / n;
-    }
-    for (int r = tid; r < p; r += kThreads) rhs[r] = G[(r + 1) * p2 + (p + 1)] - G[r + 1] * G[p + 1] / n;
-    __syncthreads();
-    for (int r = tid; r < p; r += kThreads) {
-        double d = M[r][r];
-        dsc[r] = d > 0 ? 1.0 / __builtin_sqrt(d) : 0.0;
-        drop[r] = !(d > 0);
+    for (int r = tid; r < q; r += kThreads) {
+        const double d = G[(r + 1) * p2 + r + 1] - G[r + 1] * G[r + 1] / n;
+        dsc[r] = r < p ? (d > 0 ? 1.0 / __builtin_sqrt(d) : 0.0) : 1.0;
+        if (r < p) drop[r] = !(d > 0);
     }
     __syncthreads();
-    for (int i = tid; i < p * p; i += kThreads) {
-        int r = i / p, c = i % p;
-        M[r][c] = M[r][c] * dsc[r] * dsc[c];
-    }
-    for (int r = tid; r < p; r += kThreads) rhs[r] = rhs[r] * dsc[r];
+    // lower triangle of D C D (row-major, ld = q + 1)
+    for (int r = tid >> 4; r < q; r += kThreads >> 4)
+        for (int c = tid & 15; c <= r; c += 16) {
+            const double v = G[(r + 1) * p2 + c + 1] - G[r + 1] * G[c + 1] / n;
+            M[r * ld + c] = v * dsc[r] * dsc[c];
+        }
     __syncthreads();
-    // right-looking Cholesky (lower), thresholded
+    // right-looking Cholesky of the x block, thresholded; the y row rides along
+    const int ty = tid >> 4, tx = tid & 15;
     for (int k = 0; k < p; ++k) {
-        if (tid == 0) {
-            double d = M[k][k];
-            if (drop[k] || !(d > s.tol)) {
-                drop[k] = 1;
-                piv = 0.0;
-            } else {
-                piv = __builtin_sqrt(d);
+        const double d = M[k * ld + k];
+        const bool dr = drop[k] || !(d > s.tol);     // uniform: every thread reads the same
+        if (!dr) {
+            const double inv = 1.0 / d;
+            for (int i = k + 1 + ty; i < q; i += 16) {
+                const double mik = M[i * ld + k] * inv;
+                for (int j = k + 1 + tx; j <= i; j += 16)
+                    M[i * ld + j] = M[i * ld + j] - mik * M[j * ld + k];
             }
         }
+        if (tid == 0) { drop[k] = dr ? 1 : 0; dk[k] = d; }
         __syncthreads();
-        const double pk = piv;
-        if (pk == 0.0) {
-            for (int i = tid; i < p; i += kThreads) { M[i][k] = 0.0; M[k][i] = 0.0; }
-            __syncthreads();
-            continue;
+    }
+    if (tid < 64) {                                  // back substitution, one wave
+        const int lane = tid;
+        double t0 = lane < p ? M[p * ld + lane] : 0.0;
+        double t1 = lane + 64 < p ? M[p * ld + lane + 64] : 0.0;
+        for (int k = p - 1; k >= 0; --k) {
+            const double tk = __shfl(k >= 64 ? t1 : t0, k & 63, 64);
+            const double bk = drop[k] ? 0.0 : tk / dk[k];
+            if (lane == 0) bvec[k] = bk;
+            if (lane < k) t0 = t0 - M[k * ld + lane] * bk;
+            if (lane + 64 < k) t1 = t1 - M[k * ld + lane + 64] * bk;
         }
-        for (int i = k + tid; i < p; i += kThreads) M[i][k] = (i == k) ? pk : M[i][k] / pk;
-        __syncthreads();
-        const int m = p - k - 1;
-        for (int e = tid; e < m * m; e += kThreads) {
-            int i = k + 1 + e / m, j = k + 1 + e % m;
-            if (j <= i) M[i][j] = M[i][j] - M[i][k] * M[j][k];
-        }
-        __syncthreads();
-    }
-    // forward / back substitution (sequential in k; every wave takes part in the barriers)
-    for (int k = 0; k < p; ++k) {
-        if (tid == 0) rhs[k] = drop[k] ? 0.0 : rhs[k] / M[k][k];
-        __syncthreads();
-        const double v = rhs[k];
-        for (int i = k + 1 + tid; i < p; i += kThreads) rhs[i] = rhs[i] - M[i][k] * v;
-        __syncthreads();
-    }
-    for (int k = p - 1; k >= 0; --k) {
-        if (tid == 0) rhs[k] = drop[k] ? 0.0 : rhs[k] / M[k][k];
-        __syncthreads();
-        const double v = rhs[k];
-        for (int i = tid; i < k; i += kThreads) rhs[i] = rhs[i] - M[k][i] * v;
-        __syncthreads();
-    }
-    if (tid == 0) {
-        double icpt = sf[p + 1] + mean[p + 1];           // ybar
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bvec visible to the wave
+        double part = 0.0;                           // intercept = ybar - sum xbar_j b_j
         int rk = 0;
-        for (int j = 0; j < p; ++j) {
-            double b = rhs[j] * dsc[j];
+        for (int j = lane; j < p; j += 64) {
+            const double b = bvec[j] * dsc[j];
             beta[1 + j] = b;
-            icpt = icpt - (sf[1 + j] + mean[1 + j]) * b;
+            part = part + (sf[1 + j] + mean[1 + j]) * b;
             rk += drop[j] ? 0 : 1;
         }
-        beta[0] = icpt;
-        s.rank[blockIdx.x] = rk;
+        for (int o = 32; o > 0; o >>= 1) {
+            part = part + __shfl_xor(part, o, 64);
+            rk += __shfl_xor(rk, o, 64);
+        }
+        if (lane == 0) {
+            beta[0] = (sf[p + 1] + mean[p + 1]) - part;
+            s.rank[blockIdx.x] = rk;
+        }
     }
 }
 
@@ -418,11 +408,13 @@ constexpr int kPoolBlock = 64;
 __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, const double* shift,
                                                         int p2, int64_t nseg, int64_t per,
                                                         double* out_gram, double* out_shift) {
-    extern __shared__ __attribute__((aligned(16))) double C[];   // [p2][p2]
+    extern __shared__ __attribute__((aligned(16))) double C[];   // [p2][p2], lower triangle
     __shared__ double mu[kMaxF];
     __shared__ double dl[kMaxF];
+    __shared__ double g0[kMaxF];
     __shared__ double ntot_s, fac_s;
     const int tid = threadIdx.x;
+    const int ty = tid >> 4, tx = tid & 15;
     const int q2 = p2 * p2;
     const int64_t s0 = (int64_t)blockIdx.x * per;
     const int64_t s1 = s0 + per < nseg ? s0 + per : nseg;
@@ -435,7 +427,10 @@ __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, cons
         const double* S = shift + sg * p2;
         const double nb = G[0];
         if (!(nb > 0)) continue;                       // uniform
-        if (tid < p2 && tid > 0) dl[tid] = (S[tid] + G[tid] / nb) - mu[tid];
+        if (tid < p2 && tid > 0) {
+            g0[tid] = G[tid];
+            dl[tid] = (S[tid] + G[tid] / nb) - mu[tid];
+        }
         if (tid == 0) {
             const double na = ntot_s;
             fac_s = na * nb / (na + nb);
@@ -443,22 +438,22 @@ __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, cons
         }
         __syncthreads();
         const double fac = fac_s;
-        for (int e = tid; e < q2; e += kThreads) {
-            const int r = e / p2, c = e - r * p2;
-            if (r > 0 && c > 0) {
-                const double cb = G[e] - G[r] * G[c] / nb;            // segment centered
-                C[e] = C[e] + cb + dl[r] * dl[c] * fac;
+        for (int r = 1 + ty; r < p2; r += 16)
+            for (int c = 1 + tx; c <= r; c += 16) {
+                const double cb = G[r * p2 + c] - g0[r] * g0[c] / nb;   // segment centered
+                C[r * p2 + c] = C[r * p2 + c] + cb + dl[r] * dl[c] * fac;
             }
-        }
         __syncthreads();
         if (tid < p2 && tid > 0) mu[tid] = mu[tid] + dl[tid] * (nb / ntot_s);
         __syncthreads();
     }
     double* og = out_gram + (int64_t)blockIdx.x * q2;
-    for (int e = tid; e < q2; e += kThreads) {
-        const int r = e / p2, c = e - r * p2;
-        og[e] = (r == 0 && c == 0) ? ntot_s : ((r == 0 || c == 0) ? 0.0 : C[e]);
-    }
+    for (int r = ty; r < p2; r += 16)
+        for (int c = tx; c < p2; c += 16) {
+            const double v = (r == 0 && c == 0) ? ntot_s
+                             : ((r == 0 || c == 0) ? 0.0 : (c <= r ? C[r * p2 + c] : C[c * p2 + r]));
+            og[r * p2 + c] = v;
+        }
     if (tid < p2) out_shift[(int64_t)blockIdx.x * p2 + tid] = (tid == 0) ? 0.0 : mu[tid];
 }
 
@@ -586,7 +581,11 @@ extern "C" int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double*
     AFM_CHECK_ARG(gram && shift && beta && nobs && rank, "null buffer");
     if (nseg <= 0) return AFM_OK;
     SolveArgs s{gram, shift, p, tol, beta, nobs, rank};
-    hipLaunchKernelGGL(ols_solve_kernel, dim3((unsigned)nseg), dim3(kThreads), 0, ctx->stream, s);
+    const size_t lds = sizeof(double) * (size_t)(p + 1) * (p + 2);
+    AFM_HIP(hipFuncSetAttribute((const void*)ols_solve_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(ols_solve_kernel, dim3((unsigned)nseg), dim3(kThreads), lds, ctx->stream,
+                       s);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
