@@ -26,6 +26,13 @@ namespace afm {
 namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+#ifdef AFM_FP_PROFILE
+// profiling build only: per (workgroup, wave) [total cycles, cycles waiting at barriers]
+__device__ long long g_gram_cycles[1 << 16];
+#define GPROF_BAR(acc) { const long long _t = __builtin_readcyclecounter(); lds_barrier(); acc += __builtin_readcyclecounter() - _t; }
+#else
+#define GPROF_BAR(acc) lds_barrier();
+#endif
 typedef unsigned long long u64;
 
 constexpr int kMaxTiles = 7;          // p + 2 <= 112
@@ -77,145 +84,141 @@ template <int NT>
 struct GramSmem {
     static constexpr int NF = NT * 16;
     static constexpr int NP = NT * (NT + 1) / 2;
-    // tile rows: the staged block (x features 0..NF-1 zero padded, y at row NF), reused by the
-    // epilogue for the partial sums of the second row half (pairs x 256 + border x 64)
+    static constexpr int TROWS = NF + 2;             // x rows (zero padded), y row NF, dump NF+1
+    // the epilogue reuses the tiles for the second row half's partial sums
     static constexpr int RED = NP * 256 + (2 * NT + 3) * 64;
-    static constexpr int ROWS = (NF + 2) * kRS >= RED ? NF + 2 : (RED + kRS - 1) / kRS;
-    double tile[ROWS][kRS];
-    double shs[NF + 1];
-    int rowbit[kRows];             // mask bit of row r0 + a
-    int rowbad[kRows];             // == block counter: some value of the row is non-finite
-    int64_t coff[NF + 4];          // element offset of staged feature f (f > p: y again)
-    int lrow[NF + 4];              // tile row of staged feature f (f > p: the dump row NF + 1)
+    static_assert(2 * TROWS * kRS >= RED, "epilogue scratch must fit in the tiles");
+    double tile[2][TROWS][kRS];                      // double-buffered 64-row blocks
+    double shs[NF + 2];                              // shifts of the tile rows (dump row: 0)
+    int rowbad[2][kRows];                            // == b: row of block b is masked in but non-finite
+    int anybad[2];                                   // == b: block b has such a row
+    int cnt[kRows];                                  // usable rows, per lane (producer 0)
+    int64_t coff[NF + 4];                            // element offset of staged feature f
     int found;
+    int srow;                                        // the shift row (first usable row)
+};
+
+// border sums (x, x*y) of tiles [LO, HI): split between the pair groups so that their VALU work
+// balances (group 1 also owns sum y, sum y*y)
+template <int NT, int GRP>
+struct Border {
+    static constexpr int T0 = Group<NT, 0>::TMAX < NT / 2 ? Group<NT, 0>::TMAX : NT / 2;
+    static constexpr int LO = GRP == 0 ? 0 : T0;
+    static constexpr int HI = GRP == 0 ? T0 : NT;
 };
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// barrier ordering LDS only (a __syncthreads() would also drain the producers' prefetch loads)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
-// One wave of pair group GRP, row half kh.  All four waves run the same barrier sequence.
+// One staged block for a consumer wave.  Rows the mask leaves out, and masked-in rows with a
+// non-finite value (zeroed by the producers' fix-up step), are zero in the tile.
 template <int NT, int GRP>
-__device__ void gram_body(const GramArgs& g, GramSmem<NT>& sm, const int wave, const int lane) {
+__device__ __forceinline__ void gram_block(GramSmem<NT>& sm, const int buf, const int kh, const int fi, const int kk,
+                                           d4 (&acc)[Group<NT, GRP>::NQA], double (&bs)[NT],
+                                           double (&bc)[NT], double& sy, double& syy) {
     using G = Group<NT, GRP>;
+    using B = Border<NT, GRP>;
     constexpr int NF = NT * 16;
-    constexpr int KPER = ((NF + 1) * kRows + kThreads - 1) / kThreads;
+    constexpr PairTab<NT> tab{};
+    constexpr int KS = kRows / 8;                    // k-steps per block of this row half
+    constexpr bool WY = GRP == 1 || B::HI > B::LO;
+    // fragments of k-step it: rows (kh + 2 it) * 4 + kk; two register sets in ping-pong (no
+    // copies: every VALU instruction here is issue time the MFMA pipe loses)
+    auto ld = [&](double (&f)[NT], double& y, int it) {
+        const int a = (kh + 2 * it) * 4 + kk;
+#pragma unroll
+        for (int t = 0; t < G::TMAX; ++t) f[t] = sm.tile[buf][t * 16 + fi][a];
+        if (WY) y = sm.tile[buf][NF][a];
+    };
+    auto step = [&](const double (&f)[NT], const double y) {
+#pragma unroll
+        for (int t = B::LO; t < B::HI; ++t) {
+            bs[t] = bs[t] + f[t];
+            bc[t] = __builtin_fma(f[t], y, bc[t]);
+        }
+        if (GRP == 1) {
+            sy = sy + y;
+            syy = __builtin_fma(y, y, syy);
+        }
+#pragma unroll
+        for (int q = 0; q < G::NQ; ++q)
+            acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[tab.I[G::Q0 + q]], f[tab.J[G::Q0 + q]],
+                                                          acc[q], 0, 0, 0);
+    };
+    static_assert(KS % 2 == 0, "ping-pong needs an even k-step count");
+    double fa[NT], fb[NT], ya = 0.0, yb = 0.0;
+    ld(fa, ya, 0);
+#pragma unroll
+    for (int it = 0; it < KS; it += 2) {
+        ld(fb, yb, it + 1);
+        step(fa, ya);
+        if (it + 2 < KS) ld(fa, ya, it + 2);
+        step(fb, yb);
+    }
+}
+
+// Consumer wave (MFMA): pair group GRP, row half kh = wave & 1.  Block b lives in tile[b & 1].
+template <int NT, int GRP>
+__device__ void gram_consume(const GramArgs& g, GramSmem<NT>& sm, const int wave, const int lane,
+                             const int nb) {
+    using G = Group<NT, GRP>;
+    using B = Border<NT, GRP>;
     constexpr PairTab<NT> tab{};
     const int kh = wave & 1;
     const int p = g.p;
-    const int64_t seg = g.seg0 + blockIdx.x;
-    const int64_t rowbase = seg * g.seg_stride;
-    const int tid = threadIdx.x;
-
-    // staging slots: element j of this thread = feature f = wave + 4 j (wave-uniform; f == p is
-    // y, f > p re-reads y into a dump row), row a = lane.  Rows past the segment (or the long
-    // design's row_limit) are clamped to its last row and masked out by rowbit.
-    double pre[KPER];
-    int64_t rmax = g.seg_rows - 1;
-    if (g.row_limit >= 0 && g.row_limit - 1 - rowbase < rmax) rmax = g.row_limit - 1 - rowbase;
-    auto prefetch = [&](int64_t r0) {
-        int64_t r = r0 + lane;
-        r = r < rmax ? r : rmax;
-#pragma unroll
-        for (int j = 0; j < KPER; ++j) pre[j] = g.base[sm.coff[wave + 4 * j] + r];
-    };
-    prefetch(0);
-
     d4 acc[G::NQA];
 #pragma unroll
     for (int q = 0; q < G::NQA; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
-    double bs[NT], bc[NT];          // border (GRP 1): per lane sum x, sum x*y
+    double bs[NT], bc[NT];          // border: per lane sum x, sum x*y of tiles [LO, HI)
 #pragma unroll
     for (int t = 0; t < NT; ++t) { bs[t] = 0.0; bc[t] = 0.0; }
-    double sy = 0.0, syy = 0.0, nn = 0.0;
+    double sy = 0.0, syy = 0.0;
     const int fi = lane & 15, kk = lane >> 4;
-
-    bool have_shift = false;
-    int blk = 0;
-    for (int64_t r0 = 0; r0 < g.seg_rows; r0 += kRows, ++blk) {
-        // ---- stage: mask bits, values (minus the shift once known), non-finite flags ----
-        if (tid < kRows) {
-            const int64_t r = r0 + tid;
-            bool ok = r < g.seg_rows;
-            if (ok && g.row_limit >= 0) ok = rowbase + r < g.row_limit;
-            if (ok && g.bits) ok = (g.bits[(seg >> 6) * g.seg_stride + r] >> (seg & 63)) & 1ull;
-            sm.rowbit[tid] = ok ? 1 : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < KPER; ++j) {
-            const int lr = sm.lrow[wave + 4 * j];
-            const double x = pre[j];
-            if (!__builtin_isfinite(x)) sm.rowbad[lane] = blk;       // benign race: same value
-            sm.tile[lr][lane] = x - sm.shs[lr];                       // shs = 0 until found
-        }
-        __syncthreads();
-        if (r0 + kRows < g.seg_rows) prefetch(r0 + kRows);        // in flight during the MFMAs
-        if (!have_shift) {
-            // first block with a usable row: its first usable row becomes the shift
-            if (wave == 0) {
-                const u64 m = __ballot(sm.rowbit[lane] && sm.rowbad[lane] != blk);
-                if (m != 0ull) {
-                    const int a0 = __builtin_ctzll(m);
-                    for (int f = lane; f <= NF; f += 64) sm.shs[f] = (f < p || f == NF) ? sm.tile[f][a0] : 0.0;
-                    if (lane == 0) sm.found = 1;
-                }
-            }
-            __syncthreads();
-            const bool fnd = sm.found != 0;
-            __syncthreads();
-            if (!fnd) continue;                                    // uniform
-            have_shift = true;
-#pragma unroll
-            for (int j = 0; j < KPER; ++j) {
-                const int lr = sm.lrow[wave + 4 * j];
-                sm.tile[lr][lane] = sm.tile[lr][lane] - sm.shs[lr];
-            }
-            __syncthreads();
-        }
-        // ---- MFMA over this wave's k-steps: kh, kh + 2, .. ----
-#pragma unroll 2
-        for (int it = 0; it < kRows / 8; ++it) {
-            const int a = (kh + 2 * it) * 4 + kk;
-            const bool ok = sm.rowbit[a] && sm.rowbad[a] != blk;
-            double fr[NT];
-#pragma unroll
-            for (int t = 0; t < G::TMAX; ++t) fr[t] = ok ? sm.tile[t * 16 + fi][a] : 0.0;
-            if (GRP == 1) {
-                const double yv = ok ? sm.tile[NF][a] : 0.0;
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    bs[t] = bs[t] + fr[t];
-                    bc[t] = __builtin_fma(fr[t], yv, bc[t]);
-                }
-                sy = sy + yv;
-                syy = __builtin_fma(yv, yv, syy);
-                nn = nn + (ok ? 1.0 : 0.0);
-            }
-#pragma unroll
-            for (int q = 0; q < G::NQ; ++q)
-                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[tab.I[G::Q0 + q]],
-                                                              fr[tab.J[G::Q0 + q]], acc[q], 0, 0, 0);
-        }
-        __syncthreads();
+    lds_barrier();                                   // block 0 staged
+    long long twait = 0;
+    const long long tstart = __builtin_readcyclecounter();
+    for (int b = 0; b < nb; ++b) {
+        const int buf = b & 1;
+        if (__builtin_amdgcn_readfirstlane(sm.anybad[buf]) == b) lds_barrier();   // fix-up step
+#if !defined(AFM_GRAM_SKIP) || AFM_GRAM_SKIP != 1      // experiments: producers alone
+        gram_block<NT, GRP>(sm, buf, kh, fi, kk, acc, bs, bc, sy, syy);
+#endif
+        GPROF_BAR(twait);                            // tile[buf] free, block b+1 staged
     }
+#ifdef AFM_FP_PROFILE
+    if (lane == 0 && blockIdx.x < 4096) {
+        g_gram_cycles[(blockIdx.x * 8 + wave) * 2] = __builtin_readcyclecounter() - tstart;
+        g_gram_cycles[(blockIdx.x * 8 + wave) * 2 + 1] = twait;
+    }
+#else
+    (void)tstart;
+    (void)twait;
+#endif
 
     // ---- epilogue: row half 1 parks its partials, row half 0 adds them (fixed order) ----
     const int p2 = p + 2;
     double* out = g.gram + (int64_t)blockIdx.x * p2 * p2;
-    double* red = &sm.tile[0][0] + (GRP == 0 ? 0 : Group<NT, 0>::NQ * 256);
-    double* rb = &sm.tile[0][0] + GramSmem<NT>::NP * 256;          // border partials
+    double* red = &sm.tile[0][0][0] + (GRP == 0 ? 0 : Group<NT, 0>::NQ * 256);
+    double* rb = &sm.tile[0][0][0] + GramSmem<NT>::NP * 256;       // border partials
     if (kh == 1) {
 #pragma unroll
         for (int q = 0; q < G::NQ; ++q)
 #pragma unroll
             for (int r = 0; r < 4; ++r) red[(q * 4 + r) * 64 + lane] = acc[q][r];
-        if (GRP == 1) {
 #pragma unroll
-            for (int t = 0; t < NT; ++t) { rb[t * 64 + lane] = bs[t]; rb[(NT + t) * 64 + lane] = bc[t]; }
+        for (int t = B::LO; t < B::HI; ++t) {
+            rb[t * 64 + lane] = bs[t];
+            rb[(NT + t) * 64 + lane] = bc[t];
+        }
+        if (GRP == 1) {
             rb[(2 * NT) * 64 + lane] = sy;
             rb[(2 * NT + 1) * 64 + lane] = syy;
-            rb[(2 * NT + 2) * 64 + lane] = nn;
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (kh == 0) {
 #pragma unroll
         for (int q = 0; q < G::NQ; ++q) {
@@ -231,66 +234,256 @@ __device__ void gram_body(const GramArgs& g, GramSmem<NT>& sm, const int wave, c
                 }
             }
         }
-        if (GRP == 1) {
 #pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                rb[t * 64 + lane] = bs[t] + rb[t * 64 + lane];
-                rb[(NT + t) * 64 + lane] = bc[t] + rb[(NT + t) * 64 + lane];
-            }
+        for (int t = B::LO; t < B::HI; ++t) {
+            rb[t * 64 + lane] = bs[t] + rb[t * 64 + lane];
+            rb[(NT + t) * 64 + lane] = bc[t] + rb[(NT + t) * 64 + lane];
+        }
+        if (GRP == 1) {
             rb[(2 * NT) * 64 + lane] = sy + rb[(2 * NT) * 64 + lane];
             rb[(2 * NT + 1) * 64 + lane] = syy + rb[(2 * NT + 1) * 64 + lane];
-            rb[(2 * NT + 2) * 64 + lane] = nn + rb[(2 * NT + 2) * 64 + lane];
-            lds_fence();
-            // lane group kk holds rows == kk (mod 4): sum the 4 groups in order
-            for (int f = lane; f < p; f += 64) {
-                const int t = f >> 4, c = f & 15;
-                double s = 0.0, x = 0.0;
-                for (int k4 = 0; k4 < 4; ++k4) {
-                    s = s + rb[t * 64 + k4 * 16 + c];
-                    x = x + rb[(NT + t) * 64 + k4 * 16 + c];
-                }
-                out[1 + f] = s;
-                out[(1 + f) * p2] = s;
-                out[(1 + f) * p2 + p + 1] = x;
-                out[(p + 1) * p2 + 1 + f] = x;
+        }
+        lds_fence();
+        // lane group kk holds rows == kk (mod 4): sum the 4 groups in order
+        const int fend = p < B::HI * 16 ? p : B::HI * 16;
+        for (int f = B::LO * 16 + lane; f < fend; f += 64) {
+            const int t = f >> 4, c = f & 15;
+            double s = 0.0, x = 0.0;
+            for (int k4 = 0; k4 < 4; ++k4) {
+                s = s + rb[t * 64 + k4 * 16 + c];
+                x = x + rb[(NT + t) * 64 + k4 * 16 + c];
             }
-            if (lane == 0) {
-                double s = 0.0, q = 0.0, n = 0.0;
-                for (int k4 = 0; k4 < 4; ++k4) {
-                    s = s + rb[(2 * NT) * 64 + k4 * 16];
-                    q = q + rb[(2 * NT + 1) * 64 + k4 * 16];
-                    n = n + rb[(2 * NT + 2) * 64 + k4 * 16];
-                }
-                out[0] = n;
-                out[p + 1] = s;
-                out[(p + 1) * p2] = s;
-                out[(p + 1) * p2 + p + 1] = q;
+            out[1 + f] = s;
+            out[(1 + f) * p2] = s;
+            out[(1 + f) * p2 + p + 1] = x;
+            out[(p + 1) * p2 + 1 + f] = x;
+        }
+        if (GRP == 1 && lane == 0) {
+            double s = 0.0, q = 0.0;
+            for (int k4 = 0; k4 < 4; ++k4) {
+                s = s + rb[(2 * NT) * 64 + k4 * 16];
+                q = q + rb[(2 * NT + 1) * 64 + k4 * 16];
             }
+            int n = 0;
+            for (int a = 0; a < kRows; ++a) n += sm.cnt[a];
+            out[0] = (double)n;
+            out[p + 1] = s;
+            out[(p + 1) * p2] = s;
+            out[(p + 1) * p2 + p + 1] = q;
         }
     }
 }
 
-template <int NT, int MINW>
-__global__ __launch_bounds__(kThreads, MINW) void gram_kernel(GramArgs g) {
+// Producer wave pw (0..3): features pw + 4 j of every block, global -> registers two blocks
+// ahead -> tile[b & 1] minus the shift.  A row the mask leaves out is loaded from the SHIFT row
+// instead, so it stages as exact zeros with no per-element select; a masked-in row with a
+// non-finite value is flagged (rowbad / anybad) through a NaN-propagating x*0 sum.  Only loads:
+// its prefetches are never held behind stores.  With f64 MFMA, every VALU instruction of either
+// wave of a SIMD is issue time the matrix pipe loses, so this loop is written for VALU count.
+template <int NT>
+__device__ void gram_produce(const GramArgs& g, GramSmem<NT>& sm, const int pw, const int lane,
+                             const int nb, const int64_t rmax) {
     constexpr int NF = NT * 16;
+    constexpr int KPER = (NF + 4) / 4;
+    const int64_t seg = g.seg0 + blockIdx.x;
+    const int p = g.p;
+    // per-lane constants of this wave's features f = pw + 4 j: source column, shift, tile row
+    // (source pointers and tile rows are wave-uniform: forced into SGPRs, the shifts stay VGPRs)
+    const double* src[KPER];
+    double shv[KPER];
+    auto lrow_of = [&](int j) {
+        const int f = pw + 4 * j;
+        return f < p ? f : (f == p ? NF : NF + 1);
+    };
+#pragma unroll
+    for (int j = 0; j < KPER; ++j) {
+        const int64_t o = sm.coff[pw + 4 * j];
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uint64_t)o);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uint64_t)o >> 32));
+        src[j] = g.base + (int64_t)(((uint64_t)hi << 32) | lo);
+        shv[j] = sm.shs[lrow_of(j)];
+    }
+    const uint64_t* bits = g.bits ? g.bits + (seg >> 6) * g.seg_stride : nullptr;
+    const int sb = (int)(seg & 63);
+    const unsigned srow = (unsigned)sm.srow;
+    // the mask word of a block is loaded two loads ahead of its data
+    auto bits_load = [&](int b) -> uint64_t {
+        if (!bits) return ~0ull;
+        int64_t r = (int64_t)b * kRows + lane;
+        r = r < rmax ? r : rmax;
+        return bits[r];
+    };
+    // two blocks in flight per producer; register slots are compile-time (b & 1)
+    double pre0[KPER], pre1[KPER];
+    bool ok0 = false, ok1 = false;
+    int cnt = 0;                                     // producer 0: usable rows of this lane
+    bool okp = false;                                // producer 0: mask bit of the previous block
+    auto load = [&](int b, double (&pre)[KPER], bool& ok, const uint64_t bw) {
+#if defined(AFM_GRAM_SKIP) && AFM_GRAM_SKIP == 2       // experiments: consumers alone
+        return;
+#endif
+        const int64_t r = (int64_t)b * kRows + lane;
+        ok = r <= rmax && ((bw >> sb) & 1ull);
+        const unsigned off = (ok ? (unsigned)r : srow) * 8u;
+#pragma unroll
+        for (int j = 0; j < KPER; ++j)
+            pre[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(src[j]) + off);
+    };
+    auto stage = [&](int b, const double (&pre)[KPER], const bool ok) {
+#if defined(AFM_GRAM_SKIP) && AFM_GRAM_SKIP == 2
+        return;
+#endif
+        const int buf = b & 1;
+        double* tb = &sm.tile[buf][0][0] + lane;
+        double chk = 0.0;
+#pragma unroll
+        for (int j = 0; j < KPER; ++j) {
+            const double d = pre[j] - shv[j];
+            chk = __builtin_fma(d, 0.0, chk);        // NaN iff some d is not finite
+            tb[lrow_of(j) * kRS] = d;
+        }
+        const bool bad = !(chk == 0.0);
+        if (bad) sm.rowbad[buf][lane] = b;                          // benign race: same value
+        if (__ballot(bad) != 0ull && lane == 0) sm.anybad[buf] = b;
+        if (pw == 0) {
+            // block b-1 is complete (a barrier separates the two stagings): count its rows
+            if (okp && sm.rowbad[buf ^ 1][lane] != b - 1) ++cnt;
+            okp = ok;
+        }
+    };
+    // fix-up step, only for a block with a masked-in non-finite row (never on a pipeline mask,
+    // which already excludes them): zero those rows before the consumers read the block
+    auto fixup = [&](int b) {
+        const int buf = b & 1;
+        if (__builtin_amdgcn_readfirstlane(sm.anybad[buf]) != b) return;
+        if (sm.rowbad[buf][lane] == b) {
+            double* tb = &sm.tile[buf][0][0] + lane;
+#pragma unroll
+            for (int j = 0; j < KPER; ++j) tb[lrow_of(j) * kRS] = 0.0;
+        }
+        lds_barrier();
+    };
+#ifndef AFM_GRAM_PRIO
+#define AFM_GRAM_PRIO 1
+#endif
+    // the producers are the younger half: without priority they lose every VALU arbitration to
+    // the MFMA waves of their SIMD (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+    if (AFM_GRAM_PRIO) __builtin_amdgcn_s_setprio(AFM_GRAM_PRIO);
+    uint64_t bwA = bits_load(0), bwB = bits_load(1);
+    load(0, pre0, ok0, bwA);
+    bwA = bits_load(2);
+    if (nb > 1) {
+        load(1, pre1, ok1, bwB);
+        bwB = bits_load(3);
+    }
+    stage(0, pre0, ok0);
+    if (nb > 2) {
+        load(2, pre0, ok0, bwA);
+        bwA = bits_load(4);
+    }
+    lds_barrier();                                   // block 0 staged
+    long long twait = 0;
+    const long long tstart = __builtin_readcyclecounter();
+    for (int b = 0; b < nb; b += 2) {
+        // iteration b: stage b+1 (slot 1), refill slot 1 with b+3
+        fixup(b);
+        if (b + 1 < nb) {
+            stage(b + 1, pre1, ok1);
+            if (b + 3 < nb) {
+                load(b + 3, pre1, ok1, bwB);
+                bwB = bits_load(b + 5);
+            }
+        }
+        GPROF_BAR(twait);
+        if (b + 1 >= nb) break;
+        // iteration b+1: stage b+2 (slot 0), refill slot 0 with b+4
+        fixup(b + 1);
+        if (b + 2 < nb) {
+            stage(b + 2, pre0, ok0);
+            if (b + 4 < nb) {
+                load(b + 4, pre0, ok0, bwA);
+                bwA = bits_load(b + 6);
+            }
+        }
+        GPROF_BAR(twait);
+    }
+#ifdef AFM_FP_PROFILE
+    if (lane == 0 && blockIdx.x < 4096) {
+        g_gram_cycles[(blockIdx.x * 8 + 4 + pw) * 2] = __builtin_readcyclecounter() - tstart;
+        g_gram_cycles[(blockIdx.x * 8 + 4 + pw) * 2 + 1] = twait;
+    }
+#else
+    (void)tstart;
+    (void)twait;
+#endif
+    if (pw == 0) {
+        if (okp && sm.rowbad[(nb - 1) & 1][lane] != nb - 1) ++cnt;
+        sm.cnt[lane] = cnt;
+    }
+    lds_barrier();                                   // the consumers' epilogue barrier
+}
+
+// One workgroup per segment: 4 consumer waves (2 pair groups x 2 row halves) + 4 producer
+// waves; blocks of 64 rows double-buffered in LDS, one barrier per block.
+template <int NT>
+__global__ __launch_bounds__(512, 1) void gram_kernel(GramArgs g) {
+    constexpr int NF = NT * 16;
+    constexpr int TROWS = GramSmem<NT>::TROWS;
     __shared__ GramSmem<NT> sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int p = g.p;
-    const int64_t rowbase = (g.seg0 + blockIdx.x) * g.seg_stride;
-    for (int i = tid; i < GramSmem<NT>::ROWS * kRS; i += kThreads) (&sm.tile[0][0])[i] = 0.0;
-    for (int i = tid; i < NF + 4; i += kThreads) {
-        if (i <= NF) sm.shs[i] = 0.0;
+    const int p = g.p, p2 = p + 2;
+    const int64_t seg = g.seg0 + blockIdx.x;
+    const int64_t rowbase = seg * g.seg_stride;
+    for (int i = tid; i < 2 * TROWS * kRS; i += 512) (&sm.tile[0][0][0])[i] = 0.0;
+    for (int i = tid; i < NF + 4; i += 512) {
+        if (i <= NF + 1) sm.shs[i] = 0.0;
         const int c = i < p ? g.cols[i] : g.ycol;
         sm.coff[i] = (int64_t)c * g.col_stride + rowbase;
-        sm.lrow[i] = i < p ? i : (i == p ? NF : NF + 1);
     }
-    if (tid < kRows) sm.rowbad[tid] = -1;
+    if (tid < 2 * kRows) sm.rowbad[tid >> 6][tid & 63] = -1;
+    if (tid < 2) sm.anybad[tid] = -1;
     if (tid == 0) sm.found = 0;
+    int64_t rmax = g.seg_rows - 1;                   // last row of the segment (row_limit too)
+    if (g.row_limit >= 0 && g.row_limit - 1 - rowbase < rmax) rmax = g.row_limit - 1 - rowbase;
     __syncthreads();
-    if (wave < 2) gram_body<NT, 0>(g, sm, wave, lane);
-    else gram_body<NT, 1>(g, sm, wave, lane);
-    const int p2 = p + 2;
+    // ---- the shift: first usable row (mask bit set, every staged column finite) ----
+    if (wave == 0 && rmax >= 0) {
+        int64_t srow = -1;
+        for (int64_t r0 = 0; r0 <= rmax && srow < 0; r0 += kRows) {
+            const int64_t r = r0 + lane;
+            bool cand = r <= rmax;
+            if (cand && g.bits) cand = (g.bits[(seg >> 6) * g.seg_stride + r] >> (seg & 63)) & 1ull;
+            if (cand) cand = __builtin_isfinite(g.base[sm.coff[p] + r]);
+            u64 m = __ballot(cand);
+            while (m != 0ull) {
+                const int64_t row = r0 + __builtin_ctzll(m);
+                bool bad = false;
+                for (int f = lane; f < p; f += 64) bad = bad || !__builtin_isfinite(g.base[sm.coff[f] + row]);
+                if (__ballot(bad) == 0ull) { srow = row; break; }
+                m &= m - 1;
+            }
+        }
+        if (srow >= 0) {
+            for (int f = lane; f < p; f += 64) sm.shs[f] = g.base[sm.coff[f] + srow];
+            if (lane == 0) {
+                sm.shs[NF] = g.base[sm.coff[p] + srow];
+                sm.found = 1;
+                sm.srow = (int)srow;
+            }
+        }
+    }
+    __syncthreads();
+    if (!sm.found) {                                 // no usable row: n = 0
+        double* out = g.gram + (int64_t)blockIdx.x * p2 * p2;
+        for (int e = tid; e < p2 * p2; e += 512) out[e] = 0.0;
+        if (tid < p2) g.shift[(int64_t)blockIdx.x * p2 + tid] = 0.0;
+        return;
+    }
+    const int nb = (int)((rmax + kRows) / kRows);
+    if (wave < 2) gram_consume<NT, 0>(g, sm, wave, lane, nb);
+    else if (wave < 4) gram_consume<NT, 1>(g, sm, wave, lane, nb);
+    else gram_produce<NT>(g, sm, wave - 4, lane, nb, rmax);
     if (tid < p2) {
         const double v = tid == 0 ? 0.0 : (tid <= p ? sm.shs[tid - 1] : sm.shs[NF]);
         g.shift[(int64_t)blockIdx.x * p2 + tid] = v;
@@ -546,6 +739,13 @@ __global__ __launch_bounds__(256) void fama_macbeth_kernel(const double* beta, c
 
 using namespace afm;
 
+#ifdef AFM_FP_PROFILE
+extern "C" int afm_debug_gram_cycles(long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(afm::g_gram_cycles), sizeof(long long) * n) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int afm_xs_gram_f64(afm_ctx* ctx, const double* base, int64_t col_stride,
                                int64_t seg_stride, int64_t seg_rows, int64_t row_limit,
                                const int32_t* cols, int p, int ycol, const uint64_t* bits,
@@ -559,15 +759,15 @@ extern "C" int afm_xs_gram_f64(afm_ctx* ctx, const double* base, int64_t col_str
     GramArgs g{base, col_stride, seg_stride, seg_rows, row_limit, cols, ycol, p, bits, seg0, gram,
                shift};
     const int nt = (p + 15) / 16;
-    const dim3 grid((unsigned)nseg), blk(kThreads);
+    const dim3 grid((unsigned)nseg), blk(512);
     switch (nt) {
-        case 1: hipLaunchKernelGGL((gram_kernel<1, 2>), grid, blk, 0, ctx->stream, g); break;
-        case 2: hipLaunchKernelGGL((gram_kernel<2, 2>), grid, blk, 0, ctx->stream, g); break;
-        case 3: hipLaunchKernelGGL((gram_kernel<3, 2>), grid, blk, 0, ctx->stream, g); break;
-        case 4: hipLaunchKernelGGL((gram_kernel<4, 2>), grid, blk, 0, ctx->stream, g); break;
-        case 5: hipLaunchKernelGGL((gram_kernel<5, 2>), grid, blk, 0, ctx->stream, g); break;
-        case 6: hipLaunchKernelGGL((gram_kernel<6, 2>), grid, blk, 0, ctx->stream, g); break;
-        default: hipLaunchKernelGGL((gram_kernel<7, 2>), grid, blk, 0, ctx->stream, g); break;
+        case 1: hipLaunchKernelGGL((gram_kernel<1>), grid, blk, 0, ctx->stream, g); break;
+        case 2: hipLaunchKernelGGL((gram_kernel<2>), grid, blk, 0, ctx->stream, g); break;
+        case 3: hipLaunchKernelGGL((gram_kernel<3>), grid, blk, 0, ctx->stream, g); break;
+        case 4: hipLaunchKernelGGL((gram_kernel<4>), grid, blk, 0, ctx->stream, g); break;
+        case 5: hipLaunchKernelGGL((gram_kernel<5>), grid, blk, 0, ctx->stream, g); break;
+        case 6: hipLaunchKernelGGL((gram_kernel<6>), grid, blk, 0, ctx->stream, g); break;
+        default: hipLaunchKernelGGL((gram_kernel<7>), grid, blk, 0, ctx->stream, g); break;
     }
     AFM_HIP(hipGetLastError());
     return AFM_OK;
