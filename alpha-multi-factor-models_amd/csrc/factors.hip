@@ -677,15 +677,18 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
 }
 
 // TYPES workgroups per block, each with J = 15 / TYPES job waves (job sets W[J*type + wave]) and
-// a loader wave.  TYPES = 1 (15 + 1 waves, 4 waves / SIMD) when the blocks fill the chip; more
-// when a shard has few blocks (multi-GPU): every workgroup needs its own 78-KB ring, so they run
-// one per CU.
+// a loader wave.  Every workgroup needs its own 78-KB ring, so a CU holds at most two; TYPES = 1
+// (15 + 1 waves, 4 waves / SIMD, one per CU) only when even the 3-way split would not be
+// resident at once (10k assets: 157 blocks x 3 = 471 workgroups on 256 CUs, two per CU).
 template <int TYPES>
-__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1), TYPES == 1 ? 4 : 2)
+__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1)) __attribute__((amdgpu_waves_per_eu(TYPES <= 3 ? 4 : 2)))
 void factor_panel_kernel(Args a) {
     constexpr int J = kJobSets / TYPES;
-    __shared__ Smem sm_;
-    LDS Smem* sm = (LDS Smem*)&sm_;
+    // dynamic LDS: with a static size the compiler pads the VGPR allocation of the split
+    // variants up to what it thinks the LDS occupancy allows, and two 6-wave workgroups then no
+    // longer fit one CU
+    extern __shared__ double sm_dyn[];
+    LDS Smem* sm = (LDS Smem*)sm_dyn;
     const int lane = threadIdx.x & (kLanes - 1);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int type = (int)(blockIdx.x % TYPES);
@@ -693,22 +696,27 @@ void factor_panel_kernel(Args a) {
     if (threadIdx.x < 128) sm->rtab[threadIdx.x] = 1.0 / (double)threadIdx.x;
     // (the loader's first barrier also publishes rtab)
     if (wave == J) { load_wave(a, sm, lane, block); return; }
+    // this type's partial-mask planes (keeps the type out of the job waves' registers)
+    Args at = a;
+    const int64_t po = (int64_t)type * ((a.T + 63) / 64) * a.lda;
+    at.nanpart = a.nanpart + po;
+    at.badpart = a.badpart + po;
     switch (type * J + wave) {
-        case 0: run_wave<W0>(a, sm, type, wave, lane, block); break;
-        case 1: run_wave<W1>(a, sm, type, wave, lane, block); break;
-        case 2: run_wave<W2>(a, sm, type, wave, lane, block); break;
-        case 3: run_wave<W3>(a, sm, type, wave, lane, block); break;
-        case 4: run_wave<W4>(a, sm, type, wave, lane, block); break;
-        case 5: run_wave<W5>(a, sm, type, wave, lane, block); break;
-        case 6: run_wave<W6>(a, sm, type, wave, lane, block); break;
-        case 7: run_wave<W7>(a, sm, type, wave, lane, block); break;
-        case 8: run_wave<W8>(a, sm, type, wave, lane, block); break;
-        case 9: run_wave<W9>(a, sm, type, wave, lane, block); break;
-        case 10: run_wave<W10>(a, sm, type, wave, lane, block); break;
-        case 11: run_wave<W11>(a, sm, type, wave, lane, block); break;
-        case 12: run_wave<W12>(a, sm, type, wave, lane, block); break;
-        case 13: run_wave<W13>(a, sm, type, wave, lane, block); break;
-        default: run_wave<W14>(a, sm, type, wave, lane, block); break;
+        case 0: run_wave<W0>(at, sm, 0, wave, lane, block); break;
+        case 1: run_wave<W1>(at, sm, 0, wave, lane, block); break;
+        case 2: run_wave<W2>(at, sm, 0, wave, lane, block); break;
+        case 3: run_wave<W3>(at, sm, 0, wave, lane, block); break;
+        case 4: run_wave<W4>(at, sm, 0, wave, lane, block); break;
+        case 5: run_wave<W5>(at, sm, 0, wave, lane, block); break;
+        case 6: run_wave<W6>(at, sm, 0, wave, lane, block); break;
+        case 7: run_wave<W7>(at, sm, 0, wave, lane, block); break;
+        case 8: run_wave<W8>(at, sm, 0, wave, lane, block); break;
+        case 9: run_wave<W9>(at, sm, 0, wave, lane, block); break;
+        case 10: run_wave<W10>(at, sm, 0, wave, lane, block); break;
+        case 11: run_wave<W11>(at, sm, 0, wave, lane, block); break;
+        case 12: run_wave<W12>(at, sm, 0, wave, lane, block); break;
+        case 13: run_wave<W13>(at, sm, 0, wave, lane, block); break;
+        default: run_wave<W14>(at, sm, 0, wave, lane, block); break;
     }
 }
 
@@ -787,12 +795,14 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
     const int64_t nwords = (T + 63) / 64;
     const int64_t nblk = (A + 63) / 64;
-    // workgroups per block: the most job-set splits that still fit one workgroup per CU
+    // workgroups per block: the most job-set splits whose workgroups are all resident at once.
+    // A CU holds two 78-KB rings; the split variants (6, 4 or 2 waves) fit two workgroups per CU,
+    // the unsplit one (16 waves) only one.
     int ncu = 256;
     AFM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
     int types = 1;
     for (int t : {3, 5, 15})
-        if (nblk * t <= ncu) types = t;
+        if (nblk * t <= 2 * (int64_t)ncu) types = t;
     if (const char* e = getenv("AFM_FP_TYPES")) {                 // tuning override
         const int t = atoi(e);
         if (t == 1 || t == 3 || t == 5 || t == 15) types = t;
@@ -812,14 +822,27 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     a.badpart = (GLB uint64_t*)(part + types * nwords * lda);
     a.types = types;
     const dim3 grid((unsigned)(nblk * types));
+    static bool lds_attr = false;                     // > 64 KB of dynamic LDS: opt in once
+    if (!lds_attr) {
+        const int bytes = (int)sizeof(afm::Smem);
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<1>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<3>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<5>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<15>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+        lds_attr = true;
+    }
     switch (types) {
-        case 1: hipLaunchKernelGGL(afm::factor_panel_kernel<1>, grid, dim3(64 * 16), 0,
+        case 1: hipLaunchKernelGGL(afm::factor_panel_kernel<1>, grid, dim3(64 * 16), sizeof(afm::Smem),
                                    ctx->stream, a); break;
-        case 3: hipLaunchKernelGGL(afm::factor_panel_kernel<3>, grid, dim3(64 * 6), 0,
+        case 3: hipLaunchKernelGGL(afm::factor_panel_kernel<3>, grid, dim3(64 * 6), sizeof(afm::Smem),
                                    ctx->stream, a); break;
-        case 5: hipLaunchKernelGGL(afm::factor_panel_kernel<5>, grid, dim3(64 * 4), 0,
+        case 5: hipLaunchKernelGGL(afm::factor_panel_kernel<5>, grid, dim3(64 * 4), sizeof(afm::Smem),
                                    ctx->stream, a); break;
-        default: hipLaunchKernelGGL(afm::factor_panel_kernel<15>, grid, dim3(64 * 2), 0,
+        default: hipLaunchKernelGGL(afm::factor_panel_kernel<15>, grid, dim3(64 * 2), sizeof(afm::Smem),
                                     ctx->stream, a); break;
     }
     AFM_HIP(hipGetLastError());

@@ -8,8 +8,10 @@
 #include <vector>
 #include <algorithm>
 
+template <int V>
 __global__ void probe(long long* rec, int spin_ticks) {
     extern __shared__ double buf[];
+    if (V == 1) asm volatile("" ::: "v118");         // force a 119-VGPR allocation
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     buf[threadIdx.x] = (double)threadIdx.x;          // touch the allocation
     long long t = t0;
@@ -26,14 +28,21 @@ __global__ void probe(long long* rec, int spin_ticks) {
 }
 
 int main(int argc, char** argv) {
-    const int nwg = 2048, threads = 256;
+    const int nwg = 2048;
+    const int threads = argc > 1 ? atoi(argv[1]) : 256;
+    const int vg = argc > 2 ? atoi(argv[2]) : 0;      // 1: 119 VGPRs per wave
     long long* d;
     hipMalloc(&d, sizeof(long long) * 4 * nwg);
     std::vector<long long> h(4 * nwg);
-    int sizes[] = {32768, 40960, 49152, 51200, 52224, 53248, 54272, 55296, 57344, 65536, 73728, 81920};
+    int sizes[] = {32768, 40960, 49152, 51200, 52224, 53248, 54272, 55296, 57344, 65536, 73728, 78336, 81920};
     for (int lds : sizes) {
-        hipFuncSetAttribute((const void*)probe, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        hipLaunchKernelGGL(probe, dim3(nwg), dim3(threads), lds, 0, d, 4000);
+        if (vg) {
+            hipFuncSetAttribute((const void*)probe<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            hipLaunchKernelGGL(probe<1>, dim3(nwg), dim3(threads), lds, 0, d, 4000);
+        } else {
+            hipFuncSetAttribute((const void*)probe<0>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            hipLaunchKernelGGL(probe<0>, dim3(nwg), dim3(threads), lds, 0, d, 4000);
+        }
         hipDeviceSynchronize();
         hipMemcpy(h.data(), d, sizeof(long long) * 4 * nwg, hipMemcpyDeviceToHost);
         std::map<long long, std::vector<std::pair<long long, int>>> ev;
