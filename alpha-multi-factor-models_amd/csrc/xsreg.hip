@@ -598,49 +598,91 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
 // per = 64 give the same tree for any split of the segments into 64-aligned shards (multi-GPU).
 constexpr int kPoolBlock = 64;
 
+// Each thread owns up to kPoolPer elements of the lower triangle (its centered sums live in
+// registers); the next segment's Gram entries are prefetched while the current one is merged, so
+// the per-block chain runs at two barriers per segment instead of global-load latency.
+constexpr int kPoolPer = ((kMaxF - 1) * kMaxF / 2 + kThreads - 1) / kThreads;
+
 __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, const double* shift,
                                                         int p2, int64_t nseg, int64_t per,
                                                         double* out_gram, double* out_shift) {
-    extern __shared__ __attribute__((aligned(16))) double C[];   // [p2][p2], lower triangle
+    extern __shared__ __attribute__((aligned(16))) double C[];   // [p2][p2] (epilogue only)
     __shared__ double mu[kMaxF];
     __shared__ double dl[kMaxF];
     __shared__ double g0[kMaxF];
     __shared__ double ntot_s, fac_s;
     const int tid = threadIdx.x;
-    const int ty = tid >> 4, tx = tid & 15;
     const int q2 = p2 * p2;
+    const int q = p2 - 1;                              // rows / cols 1..q of the lower triangle
+    const int nel = q * (q + 1) / 2;
     const int64_t s0 = (int64_t)blockIdx.x * per;
     const int64_t s1 = s0 + per < nseg ? s0 + per : nseg;
-    for (int e = tid; e < q2; e += kThreads) C[e] = 0.0;
+    // my elements: e = tid + k * kThreads -> (r, c), 1 <= c <= r <= q
+    int ro[kPoolPer], co[kPoolPer];
+#pragma unroll
+    for (int k = 0; k < kPoolPer; ++k) {
+        const int e = tid + k * kThreads;
+        int r = (int)((__builtin_sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+        while ((r + 1) * (r + 2) / 2 <= e) ++r;
+        while (r * (r + 1) / 2 > e) --r;
+        ro[k] = e < nel ? r + 1 : 1;
+        co[k] = e < nel ? e - r * (r + 1) / 2 + 1 : 1;
+    }
+    double acc[kPoolPer], cur[kPoolPer], nxt[kPoolPer];
+#pragma unroll
+    for (int k = 0; k < kPoolPer; ++k) acc[k] = 0.0;
     if (tid < p2) mu[tid] = 0.0;
     if (tid == 0) ntot_s = 0.0;
+    double gcur = 0.0, scur = 0.0, gnxt = 0.0, snxt = 0.0, ncur = 0.0, nnxt = 0.0;
+    auto fetch = [&](int64_t sg, double (&v)[kPoolPer], double& gr, double& sh, double& n) {
+        const double* G = gram + sg * q2;
+#pragma unroll
+        for (int k = 0; k < kPoolPer; ++k) v[k] = G[ro[k] * p2 + co[k]];
+        n = G[0];
+        if (tid < p2) {
+            gr = G[tid];
+            sh = shift[sg * p2 + tid];
+        }
+    };
+    if (s0 < s1) fetch(s0, cur, gcur, scur, ncur);
     __syncthreads();
     for (int64_t sg = s0; sg < s1; ++sg) {
-        const double* G = gram + sg * q2;
-        const double* S = shift + sg * p2;
-        const double nb = G[0];
-        if (!(nb > 0)) continue;                       // uniform
-        if (tid < p2 && tid > 0) {
-            g0[tid] = G[tid];
-            dl[tid] = (S[tid] + G[tid] / nb) - mu[tid];
-        }
-        if (tid == 0) {
-            const double na = ntot_s;
-            fac_s = na * nb / (na + nb);
-            ntot_s = na + nb;
-        }
-        __syncthreads();
-        const double fac = fac_s;
-        for (int r = 1 + ty; r < p2; r += 16)
-            for (int c = 1 + tx; c <= r; c += 16) {
-                const double cb = G[r * p2 + c] - g0[r] * g0[c] / nb;   // segment centered
-                C[r * p2 + c] = C[r * p2 + c] + cb + dl[r] * dl[c] * fac;
+        if (sg + 1 < s1) fetch(sg + 1, nxt, gnxt, snxt, nnxt);
+        const double nb = ncur;
+        if (nb > 0) {                                  // uniform
+            if (tid < p2 && tid > 0) {
+                g0[tid] = gcur;
+                dl[tid] = (scur + gcur / nb) - mu[tid];
             }
-        __syncthreads();
-        if (tid < p2 && tid > 0) mu[tid] = mu[tid] + dl[tid] * (nb / ntot_s);
-        __syncthreads();
+            if (tid == 0) {
+                const double na = ntot_s;
+                fac_s = na * nb / (na + nb);
+                ntot_s = na + nb;
+            }
+            __syncthreads();
+            const double fac = fac_s, ntot = ntot_s;   // (tid 0 rewrites them next segment)
+#pragma unroll
+            for (int k = 0; k < kPoolPer; ++k) {
+                const int r = ro[k], c = co[k];
+                const double cb = cur[k] - g0[r] * g0[c] / nb;             // segment centered
+                acc[k] = acc[k] + cb + dl[r] * dl[c] * fac;
+            }
+            __syncthreads();
+            if (tid < p2 && tid > 0) mu[tid] = mu[tid] + dl[tid] * (nb / ntot);
+        }
+#pragma unroll
+        for (int k = 0; k < kPoolPer; ++k) cur[k] = nxt[k];
+        gcur = gnxt;
+        scur = snxt;
+        ncur = nnxt;
     }
+    // (the last mu update and the accumulators are published through LDS)
+#pragma unroll
+    for (int k = 0; k < kPoolPer; ++k)
+        if (tid + k * kThreads < nel) C[ro[k] * p2 + co[k]] = acc[k];
+    __syncthreads();
     double* og = out_gram + (int64_t)blockIdx.x * q2;
+    const int ty = tid >> 4, tx = tid & 15;
     for (int r = ty; r < p2; r += 16)
         for (int c = tx; c < p2; c += 16) {
             const double v = (r == 0 && c == 0) ? ntot_s
