@@ -102,7 +102,7 @@ struct Shared {
 
 // k largest keys among candidates (key valid when cand), ties -> smaller index first.
 // Writes the selected indices, sorted (key desc, index asc), to out[0..k).
-__device__ void select_top(const RebArgs& r, Shared& sh, int64_t t, int k, bool largest, int* out) {
+__device__ __forceinline__ void select_top(const RebArgs& r, Shared& sh, int64_t t, int k, bool largest, int* out) {
     const int tid = threadIdx.x;
     const int64_t A = r.A;
     u64 prefix = 0, pmask = 0;
@@ -174,6 +174,115 @@ __device__ void select_top(const RebArgs& r, Shared& sh, int64_t t, int k, bool 
         out[rank] = mi;
     }
     __syncthreads();
+}
+
+// Radix digit choice of select_top_reg, on wave 0: the largest digit d whose suffix count
+// sum_{d' >= d} hist[d'] reaches `need` -> misc[0] = d, misc[1] = need - (count above d),
+// misc[2] = hist[d].  Lane l owns digits 4l..4l+3; a shuffle suffix scan replaces the serial
+// 256-step loop.
+__device__ __forceinline__ void digit_pick(Shared& sh, const int need) {
+    const int tid = threadIdx.x;
+    if (tid >= 64) return;
+    const int h0 = sh.hist[4 * tid], h1 = sh.hist[4 * tid + 1], h2 = sh.hist[4 * tid + 2],
+              h3 = sh.hist[4 * tid + 3];
+    const int s = h0 + h1 + h2 + h3;
+    int S = s;                                       // inclusive suffix sum over lanes
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_down(S, o, 64);
+        if (tid + o < 64) S += v;
+    }
+    const u64 m = __ballot(S >= need);
+    const int L = 63 - __clzll(m);
+    if (tid == L) {
+        int acc = S - s, d = 4 * L, hd = h0;
+        if (acc + h3 >= need) { d = 4 * L + 3; hd = h3; }
+        else if (acc + h3 + h2 >= need) { d = 4 * L + 2; hd = h2; acc += h3; }
+        else if (acc + h3 + h2 + h1 >= need) { d = 4 * L + 1; hd = h1; acc += h3 + h2; }
+        else acc += h3 + h2 + h1;
+        sh.misc[0] = d;
+        sh.misc[1] = need - acc;
+        sh.misc[2] = hd;
+    }
+}
+
+// select_top on register-resident keys: ks[j] = okey of asset j * kT + tid (0: not a candidate).
+// Same result as select_top (threshold by exact radix select; ties at the threshold taken by
+// ascending index), without re-reading the predictions for every digit.
+template <int KR>
+__device__ __forceinline__ bool select_top_reg(Shared& sh, const u64 (&ks)[KR], int k, bool largest,
+                                               int* out) {
+    const int tid = threadIdx.x;
+    u64 prefix = 0, pmask = 0;
+    int need = k, eqtot = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        sh.hist[tid] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KR; ++j) {
+            if (ks[j] != 0ull) {
+                const u64 kk = largest ? ks[j] : ~ks[j];
+                if ((kk & pmask) == prefix) atomicAdd(&sh.hist[(kk >> shift) & 255], 1);
+            }
+        }
+        __syncthreads();
+        digit_pick(sh, need);
+        __syncthreads();
+        prefix |= (u64)sh.misc[0] << shift;
+        pmask |= 255ull << shift;
+        need = sh.misc[1];
+        eqtot = sh.misc[2];
+        __syncthreads();
+    }
+    // keys > tau are all taken; of the eqtot keys == tau the `need` smallest indices (a tie
+    // straddling the threshold is rare: its indices are ranked by counting in LDS)
+    int* eqbuf = reinterpret_cast<int*>(&sh.hv[0][0]);
+    constexpr int kEqMax = (int)(sizeof(sh.hv) / sizeof(int));
+    const bool all_eq = eqtot == need;
+    if (!all_eq && eqtot > kEqMax) return false;     // (uniform) caller takes the global path
+    if (tid == 0) { sh.misc[3] = 0; sh.misc[6] = 0; }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < KR; ++j) {
+        if (ks[j] != 0ull) {
+            const u64 kk = largest ? ks[j] : ~ks[j];
+            if (kk > prefix || (all_eq && kk == prefix)) {
+                const int pos = atomicAdd(&sh.misc[3], 1);
+                sh.keysel[pos] = kk;
+                sh.idxsel[pos] = j * kT + tid;
+            } else if (kk == prefix) {
+                const int pos = atomicAdd(&sh.misc[6], 1);
+                if (pos < kEqMax) eqbuf[pos] = j * kT + tid;
+            }
+        }
+    }
+    __syncthreads();
+    if (!all_eq) {
+        const int ngt = sh.misc[3];
+        const int neq = sh.misc[6];                  // == eqtot <= kEqMax
+        for (int e = tid; e < neq; e += kT) {
+            const int me = eqbuf[e];
+            int rank = 0;
+            for (int f = 0; f < neq; ++f) rank += eqbuf[f] < me;
+            if (rank < need) {
+                sh.keysel[ngt + rank] = prefix;
+                sh.idxsel[ngt + rank] = me;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < k) {
+        const u64 mk = sh.keysel[tid];
+        const int mi = sh.idxsel[tid];
+        int rank = 0;
+        for (int j = 0; j < k; ++j) {
+            const u64 ok = sh.keysel[j];
+            const int oi = sh.idxsel[j];
+            rank += (ok > mk) || (ok == mk && oi < mi);
+        }
+        out[rank] = mi;
+    }
+    __syncthreads();
+    return true;
 }
 
 // numpy pairwise sum of a dense vector (n small)
@@ -392,26 +501,47 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
     const int64_t tn = i + 1 < r.nd ? r.dates[i + 1] : -1;
     const int nw = (int)((r.A + 63) / 64);
 
-    // ---- prediction presence rows (prev, cur, next) and candidate count --------------------
-    for (int wi = tid; wi < nw; wi += kT) {
-        u64 m[3] = {0, 0, 0};
-        const int64_t ts[3] = {tp, t, tn};
-        for (int q = 0; q < 3; ++q) {
-            if (ts[q] < 0) continue;
-            for (int b = 0; b < 64; ++b) {
-                int64_t a = (int64_t)wi * 64 + b;
-                if (a < r.A) {
-                    double v = r.pred[ts[q] * r.lda + a];
-                    if (v == v) m[q] |= 1ull << b;
+    // ---- prediction presence rows (prev, cur, next) by ballot; candidate keys of date t in
+    // registers (asset j * kT + tid) when the panel is narrow enough ---------------------------
+    constexpr int KR = 48;                           // register keys: A <= 12288
+    const bool regk = r.A <= (int64_t)KR * kT;
+    u64 ks[KR];
+#pragma unroll
+    for (int j = 0; j < KR; ++j) ks[j] = 0ull;
+    int nc = 0;
+    {
+        for (int64_t a0 = 0; a0 < (int64_t)nw * 64; a0 += kT) {
+            const int64_t a = a0 + tid;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int64_t tq = q == 0 ? tp : (q == 1 ? t : tn);
+                bool has = false;
+                if (tq >= 0 && a < r.A) {
+                    const double v = r.pred[tq * r.lda + a];
+                    has = v == v;
+                }
+                const u64 m = __ballot(has);
+                if ((tid & 63) == 0) sh.pw[q][a >> 6] = m;
+            }
+        }
+    }
+    if (regk) {
+#pragma unroll
+        for (int j = 0; j < KR; ++j) {
+            const int64_t a = (int64_t)j * kT + tid;
+            if (a < r.A) {
+                const double v = r.pred[t * r.lda + a];
+                if (v == v && bit_at(r.trad, r.lda, t, a)) {
+                    ks[j] = okey(v);
+                    ++nc;
                 }
             }
         }
-        for (int q = 0; q < 3; ++q) sh.pw[q][wi] = m[q];
-    }
-    int nc = 0;
-    for (int64_t a = tid; a < r.A; a += kT) {
-        double v = r.pred[t * r.lda + a];
-        nc += (v == v && bit_at(r.trad, r.lda, t, a)) ? 1 : 0;
+    } else {
+        for (int64_t a = tid; a < r.A; a += kT) {
+            double v = r.pred[t * r.lda + a];
+            nc += (v == v && bit_at(r.trad, r.lda, t, a)) ? 1 : 0;
+        }
     }
     int ex;
     const int ncand = block_scan(nc, sh.scan, &ex);
@@ -422,7 +552,12 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
     }
     if (tid == 0) { r.k_out[i] = k; r.status[i] = 0; }
 
-    if (k > 0) {
+    if (k > 0 && regk) {
+        if (!select_top_reg<KR>(sh, ks, k, true, sh.book[0]))
+            select_top(r, sh, t, k, true, sh.book[0]);
+        if (!select_top_reg<KR>(sh, ks, k, false, sh.book[1]))
+            select_top(r, sh, t, k, false, sh.book[1]);
+    } else if (k > 0) {
         select_top(r, sh, t, k, true, sh.book[0]);
         select_top(r, sh, t, k, false, sh.book[1]);
     }

@@ -98,3 +98,38 @@ def test_rolling_window_books_vs_oracle(top_n, window):
     assert np.abs(v - o["value"]).max() / o["value"].max() < 1e-12
     assert np.abs(np.asarray(pm.turnovers, dtype=np.float64) - o["turnover"]).max() <= \
         1e-9 * max(1.0, o["turnover"].max())
+
+
+@pytest.mark.parametrize("A,levels", [(48, 4), (300, 3), (12500, 7)])
+def test_tied_predictions_books_vs_oracle(A, levels):
+    """Predictions on a few discrete levels: the top/bottom-k threshold falls inside a tie, which
+    the engine breaks by ascending asset index, like the oracle.  A = 12500 exceeds the register
+    key capacity (12288) and takes the global-memory selection path."""
+    from afm.portfolio import PortfolioManager
+    from oracle import portfolio as P
+    rng = np.random.default_rng(A)
+    T = 130
+    top_n = 10
+    dates = np.asarray(np.busday_offset(np.datetime64("2016-01-04"), np.arange(T), roll="forward"),
+                       dtype="datetime64[ns]")
+    ids = 7 + 2 * np.arange(A)
+    present = rng.random((T, A)) < 0.95
+    tt, aa = np.nonzero(present)
+    d, i = dates[tt], ids[aa]
+    ret = rng.normal(0, 0.02, len(tt))
+    close = 50 * np.exp(rng.normal(0, 0.1, len(tt)))
+    trad = rng.random(len(tt)) < 0.9
+    hist_m = tt < 100
+    test_m = tt >= 100
+    pred_v = rng.integers(0, levels, test_m.sum()) * 0.25 - 0.5
+    pred = pd.DataFrame({"p": pred_v}, index=pd.MultiIndex.from_arrays([d[test_m], i[test_m]]))
+    hist = pd.DataFrame({"target": ret[hist_m]}, index=pd.MultiIndex.from_arrays([d[hist_m], i[hist_m]]))
+    all_df = pd.DataFrame({"in_trading_universe": np.where(trad, "Y", "N"), "close_price": close,
+                           "tmr_ret1d": ret}, index=pd.MultiIndex.from_arrays([d, i]))
+    pm = PortfolioManager(pred, hist, all_df, top_n=top_n, window=60)
+    pm.calculate_portfolio()
+    o = P.run_portfolio(d[test_m].astype(np.int64), i[test_m], pred_v,
+                        d[hist_m].astype(np.int64), i[hist_m], ret[hist_m],
+                        d.astype(np.int64), i, trad, close, ret, top_n=top_n, window=60)
+    for (dt, L, S), Lo, So in zip(pm.books, o["books"][0::2], o["books"][1::2]):
+        assert L == Lo.tolist() and S == So.tolist()
