@@ -34,6 +34,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# per-launch HBM bytes from the latest PMC passes (tools/prof_counters.sh -> tools/pmc_traffic.py;
+# FETCH_SIZE x2 and KiB corrections of MI355X_MICROARCH.md applied there)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+ROOF_KERNELS = {"factors": ("factor_panel_kernel", "masks_kernel", "labels_kernel"),
+                "xs_gram": ("gram_kernel",)}
+
+
+def pmc_traffic(stage: str, assets: int, days: int):
+    """HBM bytes per launch of the stage's kernels, or None when no PMC pass of this workload
+    is on file."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != [assets, days]:
+        return None
+    ks = d.get("kernels", {})
+    if not all(k in ks for k in ROOF_KERNELS[stage]):
+        return None
+    return sum(ks[k]["hbm_bytes"] for k in ROOF_KERNELS[stage])
+
+
 def cpu_baseline(seed: int, assets: int = 500, days: int = 2520):
     """The oracle chain (C factor restatement + numpy per-date lstsq + sklearn pooled OLS +
     numpy/Python portfolio with the exact QP), 1 core, on config A (500 assets x 2520 days)."""
@@ -160,16 +183,23 @@ def main():
         fac_gbs = FACTOR_BYTES_PER_AD * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
         gram_rows = float(pipe.nobs.sum().item()) / world      # this rank's share of the rows
         gram_tfs = gram_rows * (p + 2) * (p + 3) / (stage_ms["xs_gram"] * 1e-3) / 1e12
+        single = world == 1
         if stage_ms["factors"] >= stage_ms["xs_gram"]:
+            tb = pmc_traffic("factors", args.assets, args.days) if single else None
             roof = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(fac_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "factor_panel_kernel+labels_kernel",
+                    "unit": "GB/s", "frac": round(fac_gbs / HBM_PEAK_GBS, 4),
+                    "traffic": None if tb is None else round(tb / 1e9, 3),
+                    "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                    "algorithmic": round(FACTOR_BYTES_PER_AD * n_ad_local / 1e9, 3),
+                    "kernel": "+".join(ROOF_KERNELS["factors"]),
                     "kernel_ms": round(stage_ms["factors"], 3)}
         else:
+            tb = pmc_traffic("xs_gram", args.assets, args.days) if single else None
             roof = {"bound": "mfma", "achieved": round(gram_tfs, 2), "peak": F64_MFMA_PEAK_TFS,
                     "unit": "TFLOP/s", "frac": round(gram_tfs / F64_MFMA_PEAK_TFS, 4),
-                    "traffic": None, "kernel": "gram_kernel",
-                    "kernel_ms": round(stage_ms["xs_gram"], 3)}
+                    "traffic": None if tb is None else round(tb / 1e9, 3),
+                    "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                    "kernel": "gram_kernel", "kernel_ms": round(stage_ms["xs_gram"], 3)}
         res = {
             "metric": "asset-days/sec, factor build+XS regression+KKT (10k assets x 20y), "
                       "1/2/4/8 GPU",

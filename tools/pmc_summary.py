@@ -17,16 +17,21 @@ def short(name):
     return name.split("(")[0][:40]
 
 
-for d in sys.argv[1:]:
-    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-        agg = collections.defaultdict(lambda: collections.defaultdict(float))
-        disp = collections.defaultdict(set)
-        for r in csv.DictReader(open(f)):
-            k = short(r["Kernel_Name"])
-            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[k].add(r["Dispatch_Id"])
-        for k, v in agg.items():
-            if "native" in k or "rocclr" in k or k.startswith("void"):
-                continue
-            n = len(disp[k])
-            print(f"{d.split('/')[-1]:6s} {k:22s} x{n}", " ".join(f"{c}={x / n:.4g}" for c, x in v.items()))
+def main():
+    for d in sys.argv[1:]:
+      for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+          agg = collections.defaultdict(lambda: collections.defaultdict(float))
+          disp = collections.defaultdict(set)
+          for r in csv.DictReader(open(f)):
+              k = short(r["Kernel_Name"])
+              agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+              disp[k].add(r["Dispatch_Id"])
+          for k, v in agg.items():
+              if "native" in k or "rocclr" in k or k.startswith("void"):
+                  continue
+              n = len(disp[k])
+              print(f"{d.split('/')[-1]:6s} {k:22s} x{n}", " ".join(f"{c}={x / n:.4g}" for c, x in v.items()))
+
+
+if __name__ == "__main__":
+    main()
