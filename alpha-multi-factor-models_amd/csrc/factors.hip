@@ -79,9 +79,21 @@ struct Smem {
     double v[kRing][kLanes];   // volume ring
     double rtab[128];          // rtab[n] = 1.0 / n (IEEE), rtab[0] = +inf; indexed n & 127
     int cbyte[2][kLanes];      // presence bits of chunk c (parity c & 1), written by the loader
+    int okbyte[2][kLanes];     // 1 = every present day of chunk c has a clean window (see kClean)
     u64 nanmask[kLanes];
     u64 badmask[kLanes];       // some factor non-finite (NaN or +-inf)
 };
+
+// ---- clean windows ----------------------------------------------------------------------------
+// A present day is CLEAN when it and the kClean - 1 observations before it all have close and
+// volume in (kLo, kHi).  Over a clean day every job's inputs are finite and non-NaN (no NaN skip
+// fires, every window holds exactly W observations, close / volume / volume*close windows hold no
+// negative value, no sum or product overflows), so the pandas recurrences reduce to their
+// branch-free cores with compile-time counts.  A chunk whose present days are clean for all 64
+// lanes of the wave runs the fast step (fstep); any other chunk runs the general step.  Both
+// perform the same IEEE operations on the same states, so the results are bit-identical.
+constexpr int kClean = 58;           // ACCEL_56 reads close 57 observations back
+constexpr double kLo = 1e-50, kHi = 1e50;
 
 // x / n exactly rounded for integer 0 <= n <= 64 (Markstein: r = RN(1/n), q0 = RN(x r),
 // q = RN(q0 + (x - q0 n) r)); zero and non-finite quotients pass through (keeps -0, inf, NaN).
@@ -94,6 +106,16 @@ __device__ __forceinline__ double div_n(const LDS Smem* sm, double x, int n) {
     const double q1 = __builtin_fma(e, r, q0);
     return (q0 == 0.0 || !__builtin_isfinite(q0)) ? q0 : q1;
 }
+// The same quotient for a compile-time divisor and an x that is finite and not -0 (every clean
+// window sum, Welford increment and sum of squares: they start at +0 and RN addition never
+// yields -0 from operands that are not both -0).  For x = +0 the Markstein steps return +0.
+template <int N>
+__device__ __forceinline__ double divc(double x) {
+    constexpr double r = 1.0 / (double)N;
+    const double q0 = x * r;
+    const double e = __builtin_fma(-q0, (double)N, x);
+    return __builtin_fma(e, r, q0);
+}
 
 struct Args {
     int64_t T, lda, plane;     // plane = T * lda
@@ -104,25 +126,71 @@ struct Args {
     GLB uint64_t* nanpart;     // [types][nch][lda] per-workgroup-type "some output NaN" bits
     GLB uint64_t* badpart;     // [types][nch][lda] per-type "some output non-finite" bits
     int types;                 // workgroups per 64-asset block (1, 3, 5 or 15)
+    int fast;                  // 0: general step only (A/B tests)
+};
+
+// Ring cell of lookback L (observation p - L) as a byte offset from row 0, given pmoff = the
+// byte offset of (row pm = p mod kRing, this lane): the unsigned min of (pm - L) and
+// (pm - L + kRing) rows -- the first wraps to a huge value exactly when pm < L.
+__device__ __forceinline__ uint32_t ring_off(uint32_t pmoff, int L) {
+    const uint32_t a = pmoff - (uint32_t)(L * kLanes * 8);
+    const uint32_t b = pmoff + (uint32_t)((kRing - L) * kLanes * 8);
+    return a < b ? a : b;
+}
+
+// Per-series run of equal consecutive values (pandas roll_mean / roll_var "same value" rule):
+// identical for every window over the same series, so it is kept once per series and wave.
+struct Run {
+    double prev;
+    int same;
+    __device__ __forceinline__ void init() { prev = qnan(); same = 0; }
+    __device__ __forceinline__ void upd(double x) {          // NaN values are skipped
+        if (x == x) {
+            same = (x == prev) ? same + 1 : 1;
+            prev = x;
+        }
+    }
+    __device__ __forceinline__ void fupd(double x) {         // x known non-NaN
+        same = (x == prev) ? same + 1 : 1;
+        prev = x;
+    }
+};
+// C close, V volume, VP pinf(volume), VC pinf(volume * close), R pinf(ret), X / Y / XY the
+// rolling-corr pair (pinf(ret + 0 vol_change), pinf(vol_change + 0 ret), X * Y).
+struct Runs {
+    Run C, V, VP, VC, R, X, Y, XY;
 };
 
 // Per-lane view of one (asset, present day) step.  Lookback L reads observation p - L.
 struct Step {
     const LDS Smem* sm;
-    GLB double* out;
-    int64_t plane, cell;
-    int lane, p, pm;           // p = observation index of this day, pm = p mod kRing
+    GLB double* out;           // output row of this day: a.out + t * lda (uniform)
+    Runs* rn;
+    int64_t plane;
+    uint32_t voff, pmoff;      // asset * 8; (pm * kLanes + lane) * 8 (pm = p mod kRing)
+    int lane, p;
     bool anynan, anybad;
-    double r0;                 // ret(p), computed once per step (ret(0))
-    __device__ __forceinline__ int slot(int L) const { return pm - L + (pm < L ? kRing : 0); }
-    __device__ __forceinline__ double C(int L) const { return sm->c[slot(L)][lane]; }
-    __device__ __forceinline__ double V(int L) const { return sm->v[slot(L)][lane]; }
+    double r0, g0;             // ret(p), vol_change(p), computed once per step when needed
+    __device__ __forceinline__ double C(int L) const {
+        return *(const LDS double*)((const LDS char*)&sm->c[0][0] + ring_off(pmoff, L));
+    }
+    __device__ __forceinline__ double V(int L) const {
+        return *(const LDS double*)((const LDS char*)&sm->v[0][0] + ring_off(pmoff, L));
+    }
     __device__ __forceinline__ double div(double x, int n) const { return div_n(sm, x, n); }
+    // global_store with an SGPR base (this day's column row) and the lane's 32-bit byte offset:
+    // no per-store address arithmetic on the VALU
+    __device__ __forceinline__ void store(int col, double x) {
+        GLB double* base = out + col * plane;
+        asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(x), "s"(base));
+    }
     __device__ __forceinline__ void put(int col, double x) {
-        out[col * plane + cell] = x;
+        store(col, x);
         anynan |= (x != x);
         anybad |= !__builtin_isfinite(x);
     }
+    // fast step: columns that are finite on a clean day need no NaN / inf bookkeeping
+    __device__ __forceinline__ void putf(int col, double x) { store(col, x); }
     // close.pct_change() at lookback L, with the window kernels' inf -> NaN (_prep_values)
     __device__ __forceinline__ double ret(int L) const {
         if (L == 0) return r0;
@@ -130,22 +198,23 @@ struct Step {
         return p - L >= 1 ? r : qnan();
     }
     __device__ __forceinline__ double volchg(int L) const {
+        if (L == 0) return g0;
         const double g = V(L) / V(L + 1) - 1;
         return p - L >= 1 ? g : qnan();
     }
+    __device__ __forceinline__ double fret(int L) const { return L == 0 ? r0 : C(L) / C(L + 1) - 1; }
+    __device__ __forceinline__ double fvolchg(int L) const { return L == 0 ? g0 : V(L) / V(L + 1) - 1; }
 };
 
 // ---- pandas window kernels as register-resident recurrences -------------------------------
 // roll_mean (pandas/_libs/window/aggregations.pyx): Kahan add/remove with separate
-// compensations, same-value run rule, sign rules.  prev starts as NaN: equivalent to pandas'
-// "prev = values[0], run = 0" start for every first value.
+// compensations, same-value run rule (Run), sign rules.
 struct RollMean {
-    double sum, cadd, crem, prev;
-    int nobs, neg, same;
+    double sum, cadd, crem;
+    int nobs, neg;
     __device__ __forceinline__ void init() {
         sum = cadd = crem = 0.0;
-        prev = qnan();
-        nobs = neg = same = 0;
+        nobs = neg = 0;
     }
     __device__ __forceinline__ void add(double x) {
         if (x == x) {
@@ -154,8 +223,6 @@ struct RollMean {
             cadd = t - sum - y;
             sum = t;
             neg += __builtin_signbit(x) ? 1 : 0;
-            same = (x == prev) ? same + 1 : 1;
-            prev = x;
         }
     }
     __device__ __forceinline__ void remove(double x) {
@@ -167,32 +234,59 @@ struct RollMean {
             neg -= __builtin_signbit(x) ? 1 : 0;
         }
     }
-    __device__ __forceinline__ double result(const Step& s, int minp) const {
+    __device__ __forceinline__ double result(const Step& s, int minp, const Run& rn) const {
         if (nobs >= minp && nobs > 0) {
             double r = s.div(sum, nobs);
-            if (same >= nobs) r = prev;
+            if (rn.same >= nobs) r = rn.prev;
             else if (neg == 0 && r < 0) r = 0.0;
             else if (neg == nobs && r > 0) r = 0.0;
             return r;
         }
         return qnan();
     }
+    // clean window: the Kahan cores only (nobs stays W)
+    __device__ __forceinline__ void fremove(double x) {
+        double y = -x - crem, t = sum + y;
+        crem = t - sum - y;
+        sum = t;
+    }
+    __device__ __forceinline__ void fadd(double x) {
+        double y = x - cadd, t = sum + y;
+        cadd = t - sum - y;
+        sum = t;
+    }
+    // a window of positive values: neg = 0 < W, so only the "negative mean -> 0" rule can fire;
+    // the mean is never NaN or -0 here, so it is a max with +0
+    template <int W>
+    __device__ __forceinline__ double fresult_pos(const Run& rn) const {
+        const double r = __builtin_fmax(divc<W>(sum), 0.0);
+        return rn.same >= W ? rn.prev : r;
+    }
+    // a signed series: the sign counts are kept
+    __device__ __forceinline__ void fsigns(double xadd, double xrem) {
+        neg += (__builtin_signbit(xadd) ? 1 : 0) - (__builtin_signbit(xrem) ? 1 : 0);
+    }
+    template <int W>
+    __device__ __forceinline__ double fresult(const Run& rn) const {
+        double r = divc<W>(sum);
+        if (rn.same >= W) r = rn.prev;
+        else if (neg == 0 && r < 0) r = 0.0;
+        else if (neg == W && r > 0) r = 0.0;
+        return r;
+    }
 };
 
 // roll_var, ddof = 1: Welford with Kahan-compensated mean; the remove runs before the add.
 struct RollVar {
-    double mean, ssq, cadd, crem, prev;
-    int nobs, same;
+    double mean, ssq, cadd, crem;
+    int nobs;
     __device__ __forceinline__ void init() {
         mean = ssq = cadd = crem = 0.0;
-        prev = qnan();
-        nobs = same = 0;
+        nobs = 0;
     }
     __device__ __forceinline__ void add(const Step& s, double x) {
         if (!__builtin_isnan(x)) {
             nobs = nobs + 1;
-            same = (x == prev) ? same + 1 : 1;
-            prev = x;
             double pm = mean - cadd, y = x - cadd, t = y - mean;
             cadd = t + mean - y;
             mean = mean + s.div(t, nobs);
@@ -213,10 +307,29 @@ struct RollVar {
             }
         }
     }
-    __device__ __forceinline__ double result(const Step& s, int minp) const {
+    __device__ __forceinline__ double result(const Step& s, int minp, const Run& rn) const {
         if (nobs >= minp && nobs > 1)
-            return (same >= nobs) ? 0.0 : s.div(ssq, nobs - 1);
+            return (rn.same >= nobs) ? 0.0 : s.div(ssq, nobs - 1);
         return qnan();
+    }
+    // clean window of W: nobs W -> W - 1 -> W
+    template <int W>
+    __device__ __forceinline__ void fremove(double x) {
+        double pm = mean - crem, y = x - crem, t = y - mean;
+        crem = t + mean - y;
+        mean = mean - divc<W - 1>(t);
+        ssq = ssq - (x - pm) * (x - mean);
+    }
+    template <int W>
+    __device__ __forceinline__ void fadd(double x) {
+        double pm = mean - cadd, y = x - cadd, t = y - mean;
+        cadd = t + mean - y;
+        mean = mean + divc<W>(t);
+        ssq = ssq + (x - pm) * (x - mean);
+    }
+    template <int W>
+    __device__ __forceinline__ double fresult(const Run& rn) const {
+        return (rn.same >= W) ? 0.0 : divc<W - 1>(ssq);
     }
 };
 
@@ -249,6 +362,13 @@ struct Ewm {
         }
         return wtd;
     }
+    // clean step: the previous day was observed, so old = 1 on entry (and again on exit), wtd is
+    // not NaN (an observed day after a NaN weight resets it) and old * owf = owf; owf + nw == 1
+    __device__ __forceinline__ double fstep(double cur, double owf, double nw) {
+        const double num = owf * wtd + nw * cur;
+        wtd = (wtd != cur) ? num : wtd;
+        return wtd;
+    }
 };
 
 // alpha = 1 / (1 + com) exactly as pandas computes it (constant-folded in IEEE double)
@@ -257,14 +377,17 @@ struct SpanC {
     static constexpr double com = (SPAN - 1) / 2.0;
     static constexpr double alpha = 1.0 / (1.0 + com);
     static constexpr double owf = 1.0 - alpha;
+    static_assert(owf + alpha == 1.0, "ewm fast step needs (1 - alpha) + alpha == 1");
 };
 template <int COM>
 struct ComC {
     static constexpr double alpha = 1.0 / (1.0 + (double)COM);
     static constexpr double owf = 1.0 - alpha;
+    static_assert(owf + alpha == 1.0, "ewm fast step needs (1 - alpha) + alpha == 1");
 };
 
 // ---- jobs (one output group each; columns in No-talib.py order, see abi.cpp) --------------
+// step(): any day (pandas semantics in full); fstep(): a clean day (see kClean).
 template <int W>
 struct Sma {  // No-talib.py:9-10
     RollMean m;
@@ -272,7 +395,12 @@ struct Sma {  // No-talib.py:9-10
     __device__ void step(Step& s) {
         if (s.p >= W) m.remove(s.C(W));
         m.add(s.C(0));
-        s.put((W - 6) / 4, m.result(s, W));
+        s.put((W - 6) / 4, m.result(s, W, s.rn->C));
+    }
+    __device__ void fstep(Step& s) {
+        m.fremove(s.C(W));
+        m.fadd(s.C(0));
+        s.putf((W - 6) / 4, m.fresult_pos<W>(s.rn->C));
     }
 };
 
@@ -282,6 +410,9 @@ struct Ema {  // No-talib.py:13-14
     __device__ void init() { e.init(); }
     __device__ void step(Step& s) {
         s.put(12 + (W - 6) / 4, e.step(s.C(0), SpanC<W>::owf, SpanC<W>::alpha));
+    }
+    __device__ void fstep(Step& s) {
+        s.putf(12 + (W - 6) / 4, e.fstep(s.C(0), SpanC<W>::owf, SpanC<W>::alpha));
     }
 };
 
@@ -298,7 +429,16 @@ struct Vwma {  // No-talib.py:17-19
         const double v0 = s.V(0);
         mvc.add(pinf(v0 * s.C(0)));
         mv.add(v0);
-        s.put(24 + (W - 6) / 4, mvc.result(s, W) / mv.result(s, W));
+        s.put(24 + (W - 6) / 4, mvc.result(s, W, s.rn->VC) / mv.result(s, W, s.rn->V));
+    }
+    __device__ void fstep(Step& s) {
+        const double vq = s.V(W);
+        mvc.fremove(vq * s.C(W));
+        mv.fremove(vq);
+        mvc.fadd(s.V(0) * s.C(0));
+        mv.fadd(s.V(0));
+        // a volume mean can round to 0 -> track
+        s.put(24 + (W - 6) / 4, mvc.fresult_pos<W>(s.rn->VC) / mv.fresult_pos<W>(s.rn->V));
     }
 };
 
@@ -316,10 +456,21 @@ struct Bbands {  // No-talib.py:22-26
         double x = s.C(0);
         m.add(x);
         v.add(s, x);
-        double ma = m.result(s, W), sd = zsqrt(v.result(s, W));
+        double ma = m.result(s, W, s.rn->C), sd = zsqrt(v.result(s, W, s.rn->C));
         const int col = 36 + 2 * ((W - 14) / 6);
         s.put(col, ma + (2 * sd));
         s.put(col + 1, ma - (2 * sd));
+    }
+    __device__ void fstep(Step& s) {
+        const double xr = s.C(W), x = s.C(0);
+        m.fremove(xr);
+        v.fremove<W>(xr);
+        m.fadd(x);
+        v.fadd<W>(x);
+        const double ma = m.fresult_pos<W>(s.rn->C), sd = zsqrt(v.fresult<W>(s.rn->C));
+        const int col = 36 + 2 * ((W - 14) / 6);
+        s.putf(col, ma + (2 * sd));
+        s.putf(col + 1, ma - (2 * sd));
     }
 };
 
@@ -339,6 +490,14 @@ struct MomAccelRocr {  // No-talib.py:35-44
         s.put(60 + k, acc);
         s.put(68 + k, roc);
     }
+    __device__ void fstep(Step& s) {
+        const int k = (W - 14) / 6;
+        const double c = s.C(0), cw = s.C(W);
+        const double mom = c - cw;
+        s.putf(52 + k, mom);
+        s.putf(60 + k, mom - (s.C(1) - s.C(1 + W)));
+        s.putf(68 + k, c / cw - 1);
+    }
 };
 
 template <int SLOW>
@@ -350,6 +509,12 @@ struct Macd {  // No-talib.py:47-50
         double f = fast.step(c, SpanC<12>::owf, SpanC<12>::alpha);
         double l = slow.step(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha);
         s.put(76 + (SLOW - 18) / 6, f - l);
+    }
+    __device__ void fstep(Step& s) {
+        const double c = s.C(0);
+        const double f = fast.fstep(c, SpanC<12>::owf, SpanC<12>::alpha);
+        const double l = slow.fstep(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha);
+        s.putf(76 + (SLOW - 18) / 6, f - l);
     }
 };
 
@@ -366,6 +531,15 @@ struct Rsi {  // No-talib.py:53-59
         double ed = dn.step(w, ComC<I - 1>::owf, ComC<I - 1>::alpha);
         double rs = eu / ed;
         s.put(79 + (I - 8) / 6, 100 - (100 / (1 + rs)));
+    }
+    __device__ void fstep(Step& s) {
+        const double d = s.C(0) - s.C(1);
+        const double u = d >= 0 ? d : 0.0;
+        const double w = -(d <= 0 ? d : 0.0);
+        const double eu = up.fstep(u, ComC<I - 1>::owf, ComC<I - 1>::alpha);
+        const double ed = dn.fstep(w, ComC<I - 1>::owf, ComC<I - 1>::alpha);
+        const double rs = eu / ed;
+        s.put(79 + (I - 8) / 6, 100 - (100 / (1 + rs)));     // 0 / 0 on flat prices -> track
     }
 };
 
@@ -390,6 +564,15 @@ struct PvtObvPsy {  // No-talib.py:62-69
         ups -= (p >= 15 && s.C(14) > s.C(15)) ? 1 : 0;
         s.put(84, p >= 13 ? s.div((double)ups, 14) * 100 : qnan());
     }
+    __device__ void fstep(Step& s) {
+        const double c = s.C(0), v = s.V(0), c1 = s.C(1);
+        pvt = pvt + v * (c / c1 - 1);
+        s.put(82, pvt);                                   // an earlier inf term persists -> track
+        obv = obv + v * ((c - c1 <= 0) ? -1.0 : 1.0);
+        s.put(83, obv);
+        ups += (c > c1 ? 1 : 0) - (s.C(14) > s.C(15) ? 1 : 0);
+        s.putf(84, divc<14>((double)ups) * 100);
+    }
 };
 
 template <int W, int COL>
@@ -399,8 +582,15 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
     __device__ double step(Step& s) {
         if (s.p >= W) v.remove(s, pinf(s.ret(W)));
         v.add(s, pinf(s.ret(0)));
-        double r = zsqrt(v.result(s, W));
+        double r = zsqrt(v.result(s, W, s.rn->R));
         s.put(COL, r);
+        return r;
+    }
+    __device__ double fstep(Step& s) {
+        v.fremove<W>(s.fret(W));
+        v.fadd<W>(s.r0);
+        const double r = zsqrt(v.fresult<W>(s.rn->R));
+        s.putf(COL, r);
         return r;
     }
 };
@@ -409,6 +599,7 @@ struct RetSd3 {
     RetSd<3, 85> a;
     __device__ void init() { a.init(); }
     __device__ void step(Step& s) { a.step(s); }
+    __device__ void fstep(Step& s) { a.fstep(s); }
 };
 
 struct RetSd5x15 {  // sd_5, sd_15, sd5_15
@@ -417,6 +608,10 @@ struct RetSd5x15 {  // sd_5, sd_15, sd5_15
     __device__ void init() { a.init(); b.init(); }
     __device__ void step(Step& s) {
         double x = a.step(s), y = b.step(s);
+        s.put(88, x / y);
+    }
+    __device__ void fstep(Step& s) {
+        double x = a.fstep(s), y = b.fstep(s);
         s.put(88, x / y);
     }
 };
@@ -428,8 +623,15 @@ struct VolSd {  // volsd_W (No-talib.py:79-80)
     __device__ double step(Step& s) {
         if (s.p >= W) v.remove(s, pinf(s.V(W)));
         v.add(s, pinf(s.V(0)));
-        double r = zsqrt(v.result(s, W));
+        double r = zsqrt(v.result(s, W, s.rn->VP));
         s.put(COL, r);
+        return r;
+    }
+    __device__ double fstep(Step& s) {
+        v.fremove<W>(s.V(W));
+        v.fadd<W>(s.V(0));
+        const double r = zsqrt(v.fresult<W>(s.rn->VP));
+        s.putf(COL, r);
         return r;
     }
 };
@@ -438,6 +640,7 @@ struct VolSd3 {
     VolSd<3, 89> a;
     __device__ void init() { a.init(); }
     __device__ void step(Step& s) { a.step(s); }
+    __device__ void fstep(Step& s) { a.fstep(s); }
 };
 
 struct VolSd5x15 {
@@ -446,6 +649,10 @@ struct VolSd5x15 {
     __device__ void init() { a.init(); b.init(); }
     __device__ void step(Step& s) {
         double x = a.step(s), y = b.step(s);
+        s.put(92, x / y);
+    }
+    __device__ void fstep(Step& s) {
+        double x = a.fstep(s), y = b.fstep(s);
         s.put(92, x / y);
     }
 };
@@ -488,37 +695,72 @@ struct Corr {
         cnt += (t == t) ? 1 : 0;
         double c = (double)cnt;
         const double cf = cnt >= 1 ? s.div(c, cnt - 1) : -c;      // c / (c - 1)
-        double num = (mxy.result(s, W) - mx.result(s, W) * my.result(s, W)) * cf;
-        double den = __builtin_sqrt(vx.result(s, W) * vy.result(s, W));
+        double num = (mxy.result(s, W, s.rn->XY) - mx.result(s, W, s.rn->X) * my.result(s, W, s.rn->Y)) * cf;
+        double den = __builtin_sqrt(vx.result(s, W, s.rn->X) * vy.result(s, W, s.rn->Y));
         s.put(94 + (W == 15 ? 1 : 0), num / den);
         if (WITH_VC) s.put(93, s.volchg(0));
+    }
+    // clean: X = ret, Y = vol_change (finite), cnt = W; c / (c - 1) is the constant W / (W - 1)
+    __device__ void fstep(Step& s) {
+        const double Xr = s.fret(W), Yr = s.fvolchg(W), X = s.r0, Y = s.g0;
+        const double XYr = Xr * Yr, XY = X * Y;
+        mxy.fremove(XYr);
+        mx.fremove(Xr);
+        my.fremove(Yr);
+        vx.fremove<W>(Xr);
+        vy.fremove<W>(Yr);
+        mxy.fadd(XY);
+        mx.fadd(X);
+        my.fadd(Y);
+        vx.fadd<W>(X);
+        vy.fadd<W>(Y);
+        mxy.fsigns(XY, XYr);
+        mx.fsigns(X, Xr);
+        my.fsigns(Y, Yr);
+        constexpr double cf = (double)W / (double)(W - 1);
+        const double num = (mxy.fresult<W>(s.rn->XY) - mx.fresult<W>(s.rn->X) * my.fresult<W>(s.rn->Y)) * cf;
+        const double den = __builtin_sqrt(vx.fresult<W>(s.rn->X) * vy.fresult<W>(s.rn->Y));
+        s.put(94 + (W == 15 ? 1 : 0), num / den);
+        if (WITH_VC) s.putf(93, Y);
     }
 };
 
 // ---- job packs ------------------------------------------------------------------------------
+// Series flags: which per-step inputs / runs a pack reads.
+enum : unsigned {
+    kSerC = 1, kSerV = 2, kSerVP = 4, kSerVC = 8, kSerR = 16, kSerXY = 32,
+};
+template <class T> struct Ser { static constexpr unsigned value = 0; };
+template <int W> struct Ser<Sma<W>> { static constexpr unsigned value = kSerC; };
+template <int W> struct Ser<Bbands<W>> { static constexpr unsigned value = kSerC; };
+template <int W> struct Ser<Vwma<W>> { static constexpr unsigned value = kSerV | kSerVC; };
+template <> struct Ser<RetSd3> { static constexpr unsigned value = kSerR; };
+template <> struct Ser<RetSd5x15> { static constexpr unsigned value = kSerR; };
+template <> struct Ser<VolSd3> { static constexpr unsigned value = kSerVP; };
+template <> struct Ser<VolSd5x15> { static constexpr unsigned value = kSerVP; };
+template <int W, bool V> struct Ser<Corr<W, V>> { static constexpr unsigned value = kSerXY; };
+
 template <class... J>
 struct Pack;
 template <>
 struct Pack<> {
-    static constexpr bool kRet = false;
+    static constexpr unsigned kSer = 0;
     __device__ void init() {}
     __device__ void step(Step&) {}
+    __device__ void fstep(Step&) {}
 };
-template <class T>
-struct NeedsRet { static constexpr bool value = false; };
-template <int W, bool V>
-struct NeedsRet<Corr<W, V>> { static constexpr bool value = true; };
-template <>
-struct NeedsRet<RetSd3> { static constexpr bool value = true; };
-template <>
-struct NeedsRet<RetSd5x15> { static constexpr bool value = true; };
 template <class H, class... R>
 struct Pack<H, R...> {
-    static constexpr bool kRet = NeedsRet<H>::value || Pack<R...>::kRet;
+    static constexpr unsigned kSer = Ser<H>::value | Pack<R...>::kSer;
     H h;
     Pack<R...> r;
     __device__ void init() { h.init(); r.init(); }
     __device__ void step(Step& s) { h.step(s); r.step(s); }
+    __device__ void fstep(Step& s) {
+        h.fstep(s);
+        __builtin_amdgcn_sched_barrier(0);      // jobs one after another: bounds VGPR pressure
+        r.fstep(s);
+    }
 };
 
 // Static job partition over the 15 job waves of one workgroup (LPT on the per-job VALU count of
@@ -543,7 +785,8 @@ using W13 = Pack<Bbands<20>, Vwma<34>, MomAccelRocr<38>, Sma<46>>;
 using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>>;
 
 // The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
-// job waves (one per chunk + two at each 64-day word end).
+// job waves (one per chunk + two at each 64-day word end).  It also publishes, per lane and
+// chunk, whether every present day of the chunk is clean (kClean).
 __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane, int64_t block) {
     LDS Smem& sm = *smp;
     const int64_t asset = block * kLanes + lane;
@@ -551,6 +794,7 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
     double pc[kChunk], pv[kChunk];
     u64 vb = a.vbits[asset];
     int pmod = 0;                                   // observations before the staged chunk, mod kRing
+    int run = 0;                                    // consecutive in-range observations
     auto load = [&](int ch) {
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
@@ -565,16 +809,21 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         if (sh == 0 && ch > 0) vb = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
         const u64 cb = (vb >> sh) & 0xffull;
         int q = pmod;
+        bool ok = true;
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
             if ((cb >> j) & 1ull) {
                 sm.c[q][lane] = pc[j];
                 sm.v[q][lane] = pv[j];
                 q = q + 1 == kRing ? 0 : q + 1;
+                const bool good = pc[j] > kLo && pc[j] < kHi && pv[j] > kLo && pv[j] < kHi;
+                run = good ? run + 1 : 0;
+                ok = ok && run >= kClean;
             }
         }
         pmod = q;
         sm.cbyte[ch & 1][lane] = (int)cb;
+        sm.okbyte[ch & 1][lane] = (a.fast && ok) ? 1 : 0;
     };
     load(0);
     stage(0);
@@ -598,8 +847,12 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     const int64_t asset = block * kLanes + lane;
     const int nch = (int)((a.T + kChunk - 1) / kChunk);
     const int64_t nwords = (a.T + 63) / 64;
+    constexpr unsigned S = P::kSer;
     P jobs;
     jobs.init();
+    Runs rn;
+    rn.C.init(); rn.V.init(); rn.VP.init(); rn.VC.init();
+    rn.R.init(); rn.X.init(); rn.Y.init(); rn.XY.init();
     int pos = 0, pmod = 0;      // observations of this lane before the current chunk (and mod kRing)
     u64 nb = 0ull, fb = 0ull;   // this wave's NaN / non-finite bits of the current 64-day word
     lds_barrier();              // chunk 0 staged
@@ -612,26 +865,64 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     for (int ch = 0; ch < nch; ++ch) {
         const int sh = (ch * kChunk) & 63;                 // chunk offset inside its word
         const u64 cb = (u64)(unsigned)sm.cbyte[ch & 1][lane];
+        const bool clean = __builtin_amdgcn_ballot_w64(sm.okbyte[ch & 1][lane] == 0) == 0ull;
         const int64_t t0 = (int64_t)ch * kChunk;
         int p = pos, pm = pmod;
+        Step st;
+        st.sm = smp;
+        st.rn = &rn;
+        st.plane = a.plane;
+        st.voff = (uint32_t)(asset * 8);
+        st.lane = lane;
 #pragma unroll 1
         for (int s = 0; s < kChunk; ++s) {
             if ((cb >> s) & 1ull) {
-                Step st;
-                st.sm = smp;
-                st.out = a.out;
-                st.plane = a.plane;
-                st.cell = (t0 + s) * a.lda + asset;
-                st.lane = lane;
+                st.out = a.out + (t0 + s) * a.lda;
                 st.p = p;
-                st.pm = pm;
+                st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
                 st.anynan = false;
                 st.anybad = false;
-                if (P::kRet) {
-                    const double r = st.C(0) / st.C(1) - 1;
-                    st.r0 = p >= 1 ? r : qnan();
+                const double c0 = st.C(0), v0 = st.V(0);
+#ifdef AFM_FP_NOFASTCODE
+                if (false) {
+#else
+                if (clean) {
+#endif
+                    if (S & (kSerR | kSerXY)) st.r0 = c0 / st.C(1) - 1;
+                    if (S & kSerXY) st.g0 = v0 / st.V(1) - 1;
+                    if (S & kSerC) rn.C.fupd(c0);
+                    if (S & kSerV) rn.V.fupd(v0);
+                    if (S & kSerVP) rn.VP.fupd(v0);
+                    if (S & kSerVC) rn.VC.fupd(v0 * c0);
+                    if (S & kSerR) rn.R.fupd(st.r0);
+                    if (S & kSerXY) {
+                        rn.X.fupd(st.r0);
+                        rn.Y.fupd(st.g0);
+                        rn.XY.fupd(st.r0 * st.g0);
+                    }
+                    jobs.fstep(st);
+                } else {
+                    if (S & (kSerR | kSerXY)) {
+                        const double r = c0 / st.C(1) - 1;
+                        st.r0 = p >= 1 ? r : qnan();
+                    }
+                    if (S & kSerXY) {
+                        const double g = v0 / st.V(1) - 1;
+                        st.g0 = p >= 1 ? g : qnan();
+                    }
+                    if (S & kSerC) rn.C.upd(c0);
+                    if (S & kSerV) rn.V.upd(v0);
+                    if (S & kSerVP) rn.VP.upd(pinf(v0));
+                    if (S & kSerVC) rn.VC.upd(pinf(v0 * c0));
+                    if (S & kSerR) rn.R.upd(pinf(st.r0));
+                    if (S & kSerXY) {
+                        const double X = pinf(st.r0 + 0 * st.g0), Y = pinf(st.g0 + 0 * st.r0);
+                        rn.X.upd(X);
+                        rn.Y.upd(Y);
+                        rn.XY.upd(X * Y);
+                    }
+                    jobs.step(st);
                 }
-                jobs.step(st);
                 if (st.anynan) nb |= 1ull << (sh + s);
                 if (st.anybad) fb |= 1ull << (sh + s);
                 ++p;
@@ -669,9 +960,11 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     if (lane == 0) {
         const long long tot = __builtin_readcyclecounter() - tstart;
         const int jw = kJobSets / a.types;
-        g_wave_cycles[(blockIdx.x * jw + wave) * 3 % (1 << 16)] = tot;
-        g_wave_cycles[((blockIdx.x * jw + wave) * 3 + 1) % (1 << 16)] = twait;
-        g_wave_cycles[((blockIdx.x * jw + wave) * 3 + 2) % (1 << 16)] = treal;
+        const long long tend = (long long)__builtin_amdgcn_s_memrealtime();
+        g_wave_cycles[(blockIdx.x * jw + wave) * 4 % (1 << 16)] = tot;
+        g_wave_cycles[((blockIdx.x * jw + wave) * 4 + 1) % (1 << 16)] = twait;
+        g_wave_cycles[((blockIdx.x * jw + wave) * 4 + 2) % (1 << 16)] = treal;
+        g_wave_cycles[((blockIdx.x * jw + wave) * 4 + 3) % (1 << 16)] = tend;
     }
 #endif
 }
@@ -681,7 +974,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
 // (15 + 1 waves, 4 waves / SIMD, one per CU) only when even the 3-way split would not be
 // resident at once (10k assets: 157 blocks x 3 = 471 workgroups on 256 CUs, two per CU).
 template <int TYPES>
-__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1)) __attribute__((amdgpu_waves_per_eu(TYPES <= 3 ? 4 : 2)))
+__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1)) __attribute__((amdgpu_waves_per_eu(TYPES == 1 ? 4 : TYPES == 3 ? 3 : 2)))
 void factor_panel_kernel(Args a) {
     constexpr int J = kJobSets / TYPES;
     // dynamic LDS: with a static size the compiler pads the VGPR allocation of the split
@@ -800,8 +1093,10 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     // the unsplit one (16 waves) only one.
     int ncu = 256;
     AFM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    int types = 1;
-    for (int t : {3, 5, 15})
+    // 3 at least: the unsplit 16-wave workgroup caps the waves at 128 VGPRs, below what the job
+    // waves need for the fast step; extra 3-way workgroups simply queue for a free CU slot
+    int types = 3;
+    for (int t : {5, 15})
         if (nblk * t <= 2 * (int64_t)ncu) types = t;
     if (const char* e = getenv("AFM_FP_TYPES")) {                 // tuning override
         const int t = atoi(e);
@@ -821,6 +1116,9 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     a.nanpart = (GLB uint64_t*)part;
     a.badpart = (GLB uint64_t*)(part + types * nwords * lda);
     a.types = types;
+    a.fast = 1;
+    if (const char* e = getenv("AFM_FP_NOFAST"))                   // A/B: general step only
+        a.fast = atoi(e) ? 0 : 1;
     const dim3 grid((unsigned)(nblk * types));
     static bool lds_attr = false;                     // > 64 KB of dynamic LDS: opt in once
     if (!lds_attr) {

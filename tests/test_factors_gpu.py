@@ -93,3 +93,37 @@ def test_factor_kernel_rejects_bad_shapes():
     rc = _lib.lib().afm_factors_f64(ctx.bind_stream(), 100, 10, 60, *([None] * 8))
     assert rc != 0 and b"lda" in _lib.lib().afm_last_error()
     torch.cuda.synchronize()
+
+
+def test_clean_fast_step_matches_general_step(monkeypatch):
+    """The clean-window fast step (factors.hip kClean) and the general step give the same
+    bit-exact panel, with same-value runs, zero volumes and NaN closes planted inside otherwise
+    clean stretches (each forces the general step for ~58 observations, then the fast step
+    resumes on the carried states)."""
+    import torch
+    import afm
+    from afm.synthetic import make_panel
+    p = make_panel(256, 700, seed=11, hole_frac=0.01, listing_frac=0.2)
+    rng = np.random.default_rng(5)
+    for a in rng.choice(256, 40, replace=False):          # flat runs: the same-value rules
+        t0, n = int(rng.integers(100, 600)), int(rng.integers(3, 70))
+        p.close[t0:t0 + n, a] = p.close[t0, a]
+    for a in rng.choice(256, 10, replace=False):
+        p.volume[int(rng.integers(100, 690)), a] = 0.0
+    for a in rng.choice(256, 6, replace=False):
+        p.close[int(rng.integers(100, 690)), a] = np.nan
+    grid = afm.PanelGrid.from_panel(p)
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("AFM_FP_NOFAST", flag)
+        fin = torch.zeros_like(grid.vbits)
+        out, nanfree = afm.factor_panel(grid, finite=fin)
+        torch.cuda.synchronize()
+        outs[flag] = (out.clone(), nanfree.clone(), fin.clone())
+    assert torch.equal(outs["1"][1], outs["0"][1]) and torch.equal(outs["1"][2], outs["0"][2])
+    a, b = outs["1"][0], outs["0"][0]
+    assert torch.equal(a.isnan(), b.isnan()) and torch.equal(a.nan_to_num(0.0), b.nan_to_num(0.0))
+    assert torch.equal(a.signbit() & ~a.isnan(), b.signbit() & ~b.isnan())      # -0 vs +0 too
+    tt, aa, ref = oracle_panel(p)
+    got = b[:, torch.from_numpy(tt).cuda(), torch.from_numpy(aa).cuda()].T.cpu().numpy()
+    assert same(got, ref), mismatch_report(got, ref, afm.FACTOR_NAMES)

@@ -24,12 +24,12 @@ def main():
     torch.cuda.synchronize()
     L = _lib.lib()
     nblk = (A + 63) // 64
-    types = int(os.environ.get('AFM_FP_TYPES', '1'))
+    types = int(os.environ.get('AFM_FP_TYPES', '3'))
     jw = 15 // types
-    n = nblk * types * jw * 3
+    n = nblk * types * jw * 4
     buf = (ctypes.c_longlong * n)()
     assert L.afm_debug_wave_cycles(buf, n) == 0
-    c = np.frombuffer(buf, dtype=np.int64).reshape(nblk, types, jw, 3)
+    c = np.frombuffer(buf, dtype=np.int64).reshape(nblk, types, jw, 4)
     tot, wait = c[..., 0] / 1e6, c[..., 1] / 1e6
     print("Mcycles per wave (mean over blocks): total | barrier wait")
     for t in range(types):
@@ -38,6 +38,8 @@ def main():
     st = (c[..., 2] - c[..., 2].min()) / 1e2
     print("workgroup start (us after the first, 100 MHz clock): percentiles 0/25/50/75/90/100:",
           np.percentile(st[:, :, 0], [0, 25, 50, 75, 90, 100]).round(2))
+    dt = (c[..., 3] - c[..., 2]) * 1e-8                      # seconds (100 MHz clock)
+    print(f"shader clock estimate: {np.median(c[..., 0] / dt) / 1e9:.3f} GHz (cycles / real time)")
     print(f"max total {tot.max():.2f} Mcycles; per type max: "
           + " ".join(f"{tot[:, t].max():.2f}" for t in range(types)))
 
