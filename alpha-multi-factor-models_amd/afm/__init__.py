@@ -7,6 +7,7 @@ Drop-in Python surface (same names, arguments and results as the reference):
 * ``AlphaSignalAnalyzer(df, name, prices).run()`` -- KKT Yuliang Jiang.py:280-375
 * ``LinearRegression().fit/predict``              -- KKT:582-598 (pooled OLS)
 * ``PortfolioManager(...)``                       -- KKT:795-970
+* ``split_zscore(all_df)``                       -- KKT:424-458 (z-score + split)
 
 All compute runs in hand-written HIP kernels (libafm.so, C-ABI in include/afm.h); there is no
 CPU fallback.
@@ -17,7 +18,8 @@ from . import regression  # noqa: F401
 from .regression import LinearRegression, cross_sectional_ols  # noqa: F401
 from .analyzer import AlphaSignalAnalyzer  # noqa: F401
 from .portfolio import PortfolioManager  # noqa: F401
+from .zscore import split_zscore, zscore_grid  # noqa: F401
 
 __all__ = ["compute_factors", "factor_panel", "FACTOR_NAMES", "PanelGrid", "pack_bits",
            "unpack_bits", "LinearRegression", "cross_sectional_ols", "AlphaSignalAnalyzer",
-           "PortfolioManager"]
+           "PortfolioManager", "split_zscore", "zscore_grid"]

@@ -47,6 +47,8 @@ SIGNATURES = {
     "afm_xs_rank_f64": (I32, [P, I64, I64, P, P, P, P, P, P]),
     "afm_xs_stats_f64": (I32, [P, I64, I64, P, I64, P, P, P, P, I32, P, P, P, P]),
     "afm_xs_series_f64": (I32, [P, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
+    "afm_zscore_stats_f64": (I32, [P, P, I64, I64, I64, P, I32, P, I64, I64, P, P]),
+    "afm_zscore_apply_f64": (I32, [P, P, I64, I64, I64, P, I32, P, I64, I64, P, P, P, I64, P, P]),
 }
 
 

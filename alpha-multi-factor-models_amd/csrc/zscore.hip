@@ -1,0 +1,169 @@
+// Per-security z-score of the feature columns (KKT Yuliang Jiang.py:446-458):
+//   sigma = df_train_x.groupby('security_id').std(); mu = ....mean()           (KKT:446-447)
+//   df_*_x = ((x - mu) / sigma).replace([inf, -inf], nan).dropna()            (KKT:449-451)
+//
+// Two HBM passes over calendar-grid planes [T][lda] (lanes = consecutive assets of one date, so
+// every access is a coalesced 512-B row segment):
+//   zscore_stats_kernel  one thread per (column, asset): a sequential scan over the train dates
+//                        with pandas' group_mean (Kahan, NaN compensation reset) and group_var
+//                        (Welford, ddof = 1) recurrences, in the same row order as the groupby
+//                        (ascending date within a security).  Reads 8 B per (column, train row).
+//   zscore_apply_kernel  one thread per (asset, 64-day chunk): z = (x - mu) / sigma with IEEE
+//                        subtract and divide (no reciprocal: bit-exact with pandas), +-inf -> NaN,
+//                        and the dropna() row bits = rows with every column non-NaN.
+//                        Reads 8 B and writes 8 B per (column, row).
+// Both are HBM-bound (SURVEY §8(d) "cheap HBM pass"): algorithmic bytes per (column, row) are 8
+// (stats, train rows) and 16 (apply, applied rows).
+#include "afm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace afm {
+namespace {
+
+typedef unsigned long long u64;
+
+constexpr int kUnroll = 8;
+
+__device__ __forceinline__ double qnan() { return __builtin_nan(""); }
+
+// grid (ceil(lda / 256), K); thread = (column k = blockIdx.y, asset a)
+__global__ __launch_bounds__(256) void zscore_stats_kernel(const double* base, int64_t col_stride,
+                                                           int64_t lda, const int32_t* cols,
+                                                           const uint64_t* bits, int64_t t0,
+                                                           int64_t t1, double* mu, double* sd) {
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int k = blockIdx.y;
+    if (a >= lda) return;
+    const double* x = base + (int64_t)cols[k] * col_stride + a;
+    // group_mean: Kahan sum with the compensation reset when it turns NaN
+    double sum = 0.0, comp = 0.0;
+    // group_var: Welford
+    double mean = 0.0, m2 = 0.0;
+    int64_t nobs = 0;
+    for (int64_t c = t0 >> 6; c <= (t1 - 1) >> 6; ++c) {
+        u64 w = bits[c * lda + a];
+        const int64_t d0 = c << 6;
+        if (d0 < t0) w &= ~0ull << (t0 - d0);
+        if (t1 - d0 < 64) w &= (1ull << (t1 - d0)) - 1ull;
+        // days of this chunk in blocks of kUnroll: the loads of a block are issued together
+        for (int j0 = 0; j0 < 64; j0 += kUnroll) {
+            const u64 wb = (w >> j0) & ((1ull << kUnroll) - 1ull);
+            if (!__any(wb != 0)) continue;
+            double v[kUnroll];
+#pragma unroll
+            for (int j = 0; j < kUnroll; ++j)
+                v[j] = ((wb >> j) & 1ull) ? x[(d0 + j0 + j) * lda] : qnan();
+#pragma unroll
+            for (int j = 0; j < kUnroll; ++j) {
+                const double val = v[j];
+                if (val == val) {                       // absent rows read NaN: skipped
+                    nobs += 1;
+                    const double y = val - comp;
+                    const double t = sum + y;
+                    comp = t - sum - y;
+                    if (comp != comp) comp = 0.0;
+                    sum = t;
+                    const double old = mean;
+                    mean = mean + (val - old) / (double)nobs;
+                    m2 = m2 + (val - mean) * (val - old);
+                }
+            }
+        }
+    }
+    const double ct = (double)nobs;
+    mu[(int64_t)k * lda + a] = nobs == 0 ? qnan() : sum / ct;
+    sd[(int64_t)k * lda + a] = nobs <= 1 ? qnan() : __builtin_sqrt(m2 / (ct - 1.0));
+}
+
+// grid (ceil(lda / 256), chunks of [t0, t1)); thread = (asset a, chunk c)
+__global__ __launch_bounds__(256) void zscore_apply_kernel(const double* base, int64_t col_stride,
+                                                           int64_t lda, const int32_t* cols, int K,
+                                                           const uint64_t* bits, int64_t t0,
+                                                           int64_t t1, const double* mu,
+                                                           const double* sd, double* out,
+                                                           int64_t out_col_stride,
+                                                           const int32_t* out_cols,
+                                                           uint64_t* keep) {
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t c = (t0 >> 6) + blockIdx.y;
+    if (a >= lda) return;
+    u64 w = bits[c * lda + a];
+    const int64_t d0 = c << 6;
+    if (d0 < t0) w &= ~0ull << (t0 - d0);
+    if (t1 - d0 < 64) w &= (1ull << (t1 - d0)) - 1ull;
+    u64 bad = 0;
+    if (__any(w != 0)) {
+        const int64_t cell = d0 * lda + a;
+        for (int k = 0; k < K; ++k) {
+            const double m = mu[(int64_t)k * lda + a], s = sd[(int64_t)k * lda + a];
+            const double* x = base + (int64_t)cols[k] * col_stride + cell;
+            double* o = out + (int64_t)out_cols[k] * out_col_stride + cell;
+            for (int j0 = 0; j0 < 64; j0 += kUnroll) {
+                const u64 wb = (w >> j0) & ((1ull << kUnroll) - 1ull);
+                if (!__any(wb != 0)) continue;
+                double v[kUnroll];
+#pragma unroll
+                for (int j = 0; j < kUnroll; ++j)
+                    v[j] = ((wb >> j) & 1ull) ? x[(j0 + j) * lda] : 0.0;
+#pragma unroll
+                for (int j = 0; j < kUnroll; ++j) {
+                    if ((wb >> j) & 1ull) {
+                        double z = (v[j] - m) / s;
+                        if (__builtin_isinf(z)) z = qnan();
+                        bad |= (u64)(z != z) << (j0 + j);
+                        o[(j0 + j) * lda] = z;
+                    }
+                }
+            }
+        }
+    }
+    keep[c * lda + a] = w & ~bad;
+}
+
+}  // namespace
+}  // namespace afm
+
+using namespace afm;
+
+extern "C" int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t col_stride,
+                                    int64_t T, int64_t lda, const int32_t* cols, int K,
+                                    const uint64_t* bits, int64_t t0, int64_t t1, double* mu,
+                                    double* sd) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(base && cols && bits && mu && sd, "null buffer");
+    AFM_CHECK_ARG(lda > 0 && lda % 64 == 0 && K >= 1 && K <= 65535, "bad shape");
+    AFM_CHECK_ARG(col_stride >= T * lda, "col_stride smaller than a [T][lda] plane");
+    AFM_CHECK_ARG(0 <= t0 && t0 <= t1 && t1 <= T, "bad date range");
+    if (t0 == t1) {
+        AFM_HIP(hipMemsetAsync(mu, 0xff, sizeof(double) * K * lda, ctx->stream));   // NaN
+        AFM_HIP(hipMemsetAsync(sd, 0xff, sizeof(double) * K * lda, ctx->stream));
+        return AFM_OK;
+    }
+    dim3 grid((unsigned)((lda + 255) / 256), (unsigned)K);
+    hipLaunchKernelGGL(zscore_stats_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride,
+                       lda, cols, bits, t0, t1, mu, sd);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_zscore_apply_f64(afm_ctx* ctx, const double* base, int64_t col_stride,
+                                    int64_t T, int64_t lda, const int32_t* cols, int K,
+                                    const uint64_t* bits, int64_t t0, int64_t t1,
+                                    const double* mu, const double* sd, double* out,
+                                    int64_t out_col_stride, const int32_t* out_cols,
+                                    uint64_t* keep) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(base && cols && bits && mu && sd && out && out_cols && keep, "null buffer");
+    AFM_CHECK_ARG(lda > 0 && lda % 64 == 0 && K >= 1, "bad shape");
+    AFM_CHECK_ARG(col_stride >= T * lda && out_col_stride >= T * lda,
+                  "col_stride smaller than a [T][lda] plane");
+    AFM_CHECK_ARG(0 <= t0 && t0 <= t1 && t1 <= T, "bad date range");
+    if (t0 == t1) return AFM_OK;
+    const int64_t nch = ((t1 - 1) >> 6) - (t0 >> 6) + 1;
+    dim3 grid((unsigned)((lda + 255) / 256), (unsigned)nch);
+    hipLaunchKernelGGL(zscore_apply_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride,
+                       lda, cols, K, bits, t0, t1, mu, sd, out, out_col_stride, out_cols, keep);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}

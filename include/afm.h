@@ -172,6 +172,24 @@ int afm_xs_series_f64(afm_ctx* ctx, int64_t nd, const double* layer_mean, const 
                       double* cum_layer, double* ls, double* cum_port, double* ir,
                       double* scratch);
 
+/* ---- per-security z-score -- replaces KKT:446-458 -----------------------
+ * Column k of the K features is the plane base + cols[k] * col_stride ([T][lda], DEVICE int32
+ * cols[K]); rows = grid cells with a set bit in bits [ceil(T/64)][lda] (the all_df rows).
+ * Stats over the dates [t0, t1) (the train split): mu[k][lda] = groupby mean (Kahan),
+ * sd[k][lda] = groupby std (Welford, ddof=1); NaN values are skipped, no rows -> NaN. */
+int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t T,
+                         int64_t lda, const int32_t* cols, int K, const uint64_t* bits,
+                         int64_t t0, int64_t t1, double* mu, double* sd);
+/* Over the rows of [t0, t1): z = (x - mu) / sd (IEEE), +-inf -> NaN, written to the plane
+ * out + out_cols[k] * out_col_stride (out may alias base: in place when out_cols == cols);
+ * other cells are not written.  keep [ceil(T/64)][lda]: the row bits of [t0, t1) with every z
+ * non-NaN (the dropna() of KKT:449-451); every word of the chunks t0>>6 .. (t1-1)>>6 is
+ * written, bits outside [t0, t1) cleared. */
+int afm_zscore_apply_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t T,
+                         int64_t lda, const int32_t* cols, int K, const uint64_t* bits,
+                         int64_t t0, int64_t t1, const double* mu, const double* sd, double* out,
+                         int64_t out_col_stride, const int32_t* out_cols, uint64_t* keep);
+
 #ifdef __cplusplus
 }
 #endif
