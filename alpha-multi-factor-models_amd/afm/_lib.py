@@ -41,6 +41,8 @@ SIGNATURES = {
     "afm_rebalance_f64": (I32, [P, I64, I64, I64, P, I64, P, P, P, P, I64, I64, I64, P, P, I32,
                                 DBL, DBL, P, P, P, P, P, P, P]),
     "afm_pnl_scan_f64": (I32, [P, I64, P, P, P, P, P, DBL, DBL, P, P, P, P]),
+    "afm_bootstrap_pnl_f64": (I32, [P, I64, P, I64, P, P, P, P, I64, I64, P, DBL, DBL, P, P, P,
+                                    P]),
     "afm_min_variance_weights_f64": (I32, [P, P, I64, I64, I32, DBL, DBL, P, P, P]),
     "afm_fwd_returns_f64": (I32, [P, I64, I64, P, P, P]),
     "afm_xs_prepare_f64": (I32, [P, I64, I64, I64, P, P, P, P, P, P]),

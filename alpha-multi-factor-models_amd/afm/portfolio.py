@@ -77,6 +77,37 @@ def pnl_scan(reb: dict, v0: float = V0, rate: float = 1e-4):
     return res
 
 
+def bootstrap_paths(nd: int, n_paths: int = 1024, steps: int | None = None, seed: int = 2023):
+    """Rebalance-date slots drawn with replacement (BASELINE config E): int32 [n_paths][steps]."""
+    steps = nd if steps is None else steps
+    return np.random.default_rng(seed).integers(0, nd, size=(n_paths, steps)).astype(np.int32)
+
+
+def bootstrap_pnl(reb: dict, pred, dates_idx, paths, v0: float = V0, rate: float = 1e-4):
+    """Config E: the value/turnover recursion (KKT:864-892) over every bootstrap path of book
+    slots (``paths`` [npaths][steps] into the dates of ``reb``), one workgroup per path ->
+    dict of device tensors value [npaths][steps+1], turnover / long_ret / short_ret
+    [npaths][steps]."""
+    import torch
+    dev = reb["k"].device
+    paths = torch.as_tensor(np.asarray(paths, dtype=np.int32) if not torch.is_tensor(paths)
+                            else paths, device=dev).to(torch.int32).contiguous()
+    npaths, steps = int(paths.shape[0]), int(paths.shape[1])
+    nd = int(reb["k"].numel())
+    res = {"value": torch.empty((npaths, steps + 1), dtype=torch.float64, device=dev),
+           "turnover": torch.empty((npaths, steps), dtype=torch.float64, device=dev),
+           "long_ret": torch.empty((npaths, steps), dtype=torch.float64, device=dev),
+           "short_ret": torch.empty((npaths, steps), dtype=torch.float64, device=dev)}
+    ctx = _lib.Context.get(dev.index)
+    P = _lib.ptr
+    _lib.check(_lib.lib().afm_bootstrap_pnl_f64(
+        ctx.bind_stream(), int(pred.shape[1]), P(dates_idx), nd, P(pred), P(reb["k"]),
+        P(reb["books"]), P(reb["sums"]), npaths, steps, P(paths), float(v0), float(rate),
+        P(res["value"]), P(res["turnover"]), P(res["long_ret"]), P(res["short_ret"])),
+        "afm_bootstrap_pnl_f64")
+    return res
+
+
 def min_variance_weights(returns, lo: float = 0.0, hi: float = 0.1):
     """determine_weights for one book: returns [rows][k] (NaN = missing) -> (w[k], cov[k][k])."""
     import torch
@@ -201,6 +232,23 @@ class PortfolioManager:
             pos[L] = size / sm[2]
             pos[S] = -size / sm[3]
             self.current_positions = pos
+
+    def bootstrap(self, n_paths: int = 1024, steps: int | None = None, seed: int = 2023,
+                  paths=None):
+        """Extension (BASELINE config E): re-run the rebalance loop over ``n_paths`` bootstrap
+        resamples (with replacement) of the rebalance dates.  Books and weights per date are
+        those of ``calculate_portfolio``; each path has its own turnover and value recursion.
+        Returns (paths [n_paths][steps] indices into the sorted rebalance dates, dict of numpy
+        arrays value [n_paths][steps+1], turnover, long_ret, short_ret [n_paths][steps])."""
+        g = self._grid()
+        reb = rebalance(g["pred"], g["tbits"], g["hist"], g["hbits"], g["close"], g["tmr"],
+                        g["rdates"], A=g["A"], top_n=self.top_n, window=self.window, lo=self.lo,
+                        hi=self.hi)
+        nd = int(reb["k"].numel())
+        if paths is None:
+            paths = bootstrap_paths(nd, n_paths, steps, seed)
+        res = bootstrap_pnl(reb, g["pred"], g["rdates"], paths, V0, self.trading_cost_rate)
+        return np.asarray(paths), {k: v.cpu().numpy() for k, v in res.items()}
 
     def calculate_sharpe_ratio(self):                                    # KKT:894-897
         import pandas as pd

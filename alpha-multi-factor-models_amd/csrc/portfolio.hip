@@ -729,11 +729,15 @@ __device__ int build_dag(Dag& d, const int* pos, int64_t lo, int64_t n, int b, i
     return dag_add(d, L, R);
 }
 
+// Steps i are grouped in sequences of `seq` (one bootstrap path each; seq = nd for the plain
+// rebalance sequence); the book of step i is book slot ix(i) (idx = nullptr: slot i).  upos /
+// usize are per step.
 __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const int32_t* k_out,
                                                             const int32_t* books,
                                                             const int32_t* upos,
                                                             const int64_t* usize, int32_t* rec,
-                                                            int32_t* rlen) {
+                                                            int32_t* rlen, const int32_t* idx,
+                                                            int64_t seq) {
     __shared__ Dag dag;
     __shared__ int pos_s[kMaxTerms], code_s[kMaxTerms], pos_o[kMaxTerms], code_o[kMaxTerms];
     __shared__ int newid[kMaxTerms], lcount[kMaxLevels + 1];
@@ -743,31 +747,33 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
     int32_t* R = rec + i * kRec;
     if (tid == 0) cnt = 0;
     __syncthreads();
-    const bool active = i > 0 && k_out[i - 1] > 0;   // current_positions.dropna().empty -> 0
+    const int64_t si = idx ? idx[i] : i;             // book slots of this and the previous step
+    const int64_t sp = i % seq == 0 ? -1 : (idx ? idx[i - 1] : i - 1);
+    const bool active = sp >= 0 && k_out[sp] > 0;    // current_positions.dropna().empty -> 0
     if (active) {
-        const int k = k_out[i], kp = k_out[i - 1];
+        const int k = k_out[si], kp = k_out[sp];
         for (int e = tid; e < 2 * kp; e += 64) {     // previous members predicted today
             const int side = e / kp, q = e % kp;
-            const int a = books[((i - 1) * 2 + side) * kMaxK + q];
+            const int a = books[(sp * 2 + side) * kMaxK + q];
             const int pz = upos[(((i - 1) * 2 + side) * 2 + 1) * kMaxK + q];
             if (pz < 0) continue;
             int ns = 2;
             for (int s2 = 0; s2 < 2; ++s2)
                 for (int q2 = 0; q2 < k; ++q2)
-                    if (books[(i * 2 + s2) * kMaxK + q2] == a) ns = s2;
+                    if (books[(si * 2 + s2) * kMaxK + q2] == a) ns = s2;
             const int slot = atomicAdd(&cnt, 1);
             pos_s[slot] = pz;
             code_s[slot] = side * 3 + ns;
         }
         for (int e = tid; e < 2 * k; e += 64) {      // today's members predicted yesterday only
             const int side = e / k, q = e % k;
-            const int a = books[(i * 2 + side) * kMaxK + q];
+            const int a = books[(si * 2 + side) * kMaxK + q];
             const int pz = upos[((i * 2 + side) * 2 + 0) * kMaxK + q];
             if (pz < 0) continue;
             bool inprev = false;
             for (int s2 = 0; s2 < 2; ++s2)
                 for (int q2 = 0; q2 < kp; ++q2)
-                    if (books[((i - 1) * 2 + s2) * kMaxK + q2] == a) inprev = true;
+                    if (books[(sp * 2 + s2) * kMaxK + q2] == a) inprev = true;
             if (inprev) continue;
             const int slot = atomicAdd(&cnt, 1);
             pos_s[slot] = pz;
@@ -825,11 +831,13 @@ __device__ __forceinline__ void lds_sync() {
 
 // One workgroup of 2 waves.  Wave 1 stages chunk c+1 (records + sums) into LDS while wave 0
 // runs chunk c; one barrier per chunk.  Wave 0 keeps V / V_prev replicated in every lane.
+// Workgroup b scans the steps [b * nd, (b + 1) * nd) (bootstrap path b; one workgroup for the
+// plain sequence); the sums of step i are those of book slot ix(i).
 __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double* sums,
                                                       const int32_t* rec, const int32_t* rlen,
                                                       double v0, double rate, double* value,
                                                       double* turnover, double* long_ret,
-                                                      double* short_ret) {
+                                                      double* short_ret, const int32_t* idx) {
     __shared__ int buf[2][kBufWords];
     __shared__ int offs[2][kChunkDates];
     __shared__ double sm[2][kChunkDates + 1][4];
@@ -837,6 +845,14 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
     __shared__ int ccount[2];
     __shared__ double node[2 * kMaxTerms];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t base = (int64_t)blockIdx.x * nd;
+    rec += base * kRec;
+    rlen += base;
+    if (idx) idx += base;
+    value += (int64_t)blockIdx.x * (nd + 1);
+    turnover += base;
+    long_ret += base;
+    short_ret += base;
 
     // loader (wave 1): stage the dates [i0, i0 + c) into buffer b; returns i0 + c
     auto stage = [&](int64_t i0, int b) -> int64_t {
@@ -858,7 +874,7 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
         }
         for (int e = lane; e < (c + 1) * 4; e += 64) {
             const int64_t ii = i0 - 1 + e / 4;
-            sm[b][e / 4][e % 4] = ii >= 0 ? sums[ii * 4 + e % 4] : 0.0;
+            sm[b][e / 4][e % 4] = ii >= 0 ? sums[(idx ? (int64_t)idx[ii] : ii) * 4 + e % 4] : 0.0;
         }
         if (lane == 0) { cstart[b] = i0; ccount[b] = c; }
         return i0 + c;
@@ -929,6 +945,78 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
     }
 }
 
+// ---- bootstrap paths (BASELINE config E) ------------------------------------------------------
+// A path is a sequence of rebalance-date slots drawn with replacement; each step re-runs the
+// calculate_portfolio update of KKT:842-892 on the slot's date.  Books, weights and PnL sums are
+// per date (path-independent) and come from rebalance_kernel; only the turnover alignment --
+// the union of the previous and the current step's prediction sets (KKT:839) -- and the value
+// recursion depend on the path.
+
+// pbits[d][w] = prediction presence (non-NaN) of the assets 64w .. 64w+63 on rebalance slot d.
+// One wave per (slot, word): a ballot over a coalesced 512-B row segment.
+__global__ __launch_bounds__(256) void pred_bits_kernel(int64_t lda, const int32_t* dates,
+                                                       int64_t nd, const double* pred,
+                                                       uint64_t* pbits) {
+    const int64_t nw = lda >> 6;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t d = blockIdx.y;
+    if (w >= nw) return;
+    const double v = pred[(int64_t)dates[d] * lda + w * 64 + (threadIdx.x & 63)];
+    const u64 b = __ballot(v == v);
+    if ((threadIdx.x & 63) == 0) pbits[d * nw + w] = b;
+}
+
+// One wave per step i (> 0 within its path): union U = P(prev) | P(cur) word by word, a wave
+// prefix scan of the popcounts, then the union position of every book member that is also
+// predicted on the other step (the pair enters the turnover; others align with NaN and drop).
+// Writes upos[i][side][0][*] (current members), upos[i-1][side][1][*] (previous members) and
+// usize[i][0] = |U| -- the layout turnover_terms_kernel reads.
+__global__ __launch_bounds__(64) void pair_union_kernel(int64_t steps, const int32_t* path,
+                                                       int64_t nw, const uint64_t* pbits,
+                                                       const int32_t* k_out,
+                                                       const int32_t* books, int32_t* upos,
+                                                       int64_t* usize) {
+    __shared__ int prefix[kMaxWords];
+    const int64_t i = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (i % steps == 0) {
+        if (lane == 0) usize[i * 2] = 0;
+        return;
+    }
+    const int64_t dp = path[i - 1], dc = path[i];
+    const uint64_t* Pp = pbits + dp * nw;
+    const uint64_t* Pc = pbits + dc * nw;
+    int carry = 0;
+    for (int64_t w0 = 0; w0 < nw; w0 += 64) {
+        const int64_t w = w0 + lane;
+        const int c = w < nw ? __popcll(Pp[w] | Pc[w]) : 0;
+        int incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int x = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += x;
+        }
+        if (w < nw) prefix[w] = carry + incl - c;
+        carry += __shfl(incl, 63, 64);
+    }
+    __syncthreads();
+    if (lane == 0) usize[i * 2] = carry;
+    auto pos_of = [&](int a, const uint64_t* other) -> int {
+        const int wa = a >> 6, ba = a & 63;
+        if (!((other[wa] >> ba) & 1ull)) return -1;
+        const u64 lowm = ba ? ((1ull << ba) - 1ull) : 0ull;
+        return prefix[wa] + __popcll((Pp[wa] | Pc[wa]) & lowm);
+    };
+    const int kp = k_out[dp], k = k_out[dc];
+    for (int e = lane; e < 2 * kp; e += 64) {
+        const int side = e / kp, q = e % kp;
+        upos[(((i - 1) * 2 + side) * 2 + 1) * kMaxK + q] = pos_of(books[(dp * 2 + side) * kMaxK + q], Pc);
+    }
+    for (int e = lane; e < 2 * k; e += 64) {
+        const int side = e / k, q = e % k;
+        upos[((i * 2 + side) * 2 + 0) * kMaxK + q] = pos_of(books[(dc * 2 + side) * kMaxK + q], Pp);
+    }
+}
+
 }  // namespace
 }  // namespace afm
 
@@ -973,10 +1061,10 @@ extern "C" int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out,
     int32_t* rec = work;
     int32_t* rlen = work + nd * kRec;
     hipLaunchKernelGGL(turnover_terms_kernel, dim3((unsigned)nd), dim3(64), 0, ctx->stream, nd,
-                       k_out, books, upos, usize, rec, rlen);
+                       k_out, books, upos, usize, rec, rlen, (const int32_t*)nullptr, nd);
     AFM_HIP(hipGetLastError());
     hipLaunchKernelGGL(pnl_scan_kernel, dim3(1), dim3(128), 0, ctx->stream, nd, sums, rec, rlen, v0,
-                       rate, value, turnover, long_ret, short_ret);
+                       rate, value, turnover, long_ret, short_ret, (const int32_t*)nullptr);
     AFM_HIP(hipGetLastError());
     AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;
@@ -994,5 +1082,46 @@ extern "C" int afm_min_variance_weights_f64(afm_ctx* ctx, const double* R, int64
     hipLaunchKernelGGL(weights_kernel, dim3(1), dim3(kT), smem, ctx->stream, R, rows, ld, k, lo,
                        hi, w, cov, status);
     AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_bootstrap_pnl_f64(afm_ctx* ctx, int64_t lda, const int32_t* dates, int64_t nd,
+                                     const double* pred, const int32_t* k_out,
+                                     const int32_t* books, const double* sums, int64_t npaths,
+                                     int64_t steps, const int32_t* path, double v0, double rate,
+                                     double* value, double* turnover, double* long_ret,
+                                     double* short_ret) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(dates && pred && k_out && books && sums && path && value && turnover &&
+                      long_ret && short_ret, "null buffer");
+    AFM_CHECK_ARG(lda > 0 && lda % 64 == 0 && lda / 64 <= kMaxWords, "bad lda (max 32768 assets)");
+    AFM_CHECK_ARG(nd > 0 && npaths >= 0 && steps >= 0 && npaths <= 0x7fffffff, "bad sizes");
+    const int64_t n = npaths * steps;
+    if (n == 0) return AFM_OK;
+    AFM_CHECK_ARG(n <= 0x7fffffff, "npaths * steps too large for one launch");
+    const int64_t nw = lda / 64;
+    // scratch: pbits [nd][nw] u64, upos [n][2][2][kMaxK], usize [n][2], rec [n][kRec], rlen [n]
+    const size_t b_pb = sizeof(uint64_t) * nd * nw, b_up = sizeof(int32_t) * n * 4 * kMaxK,
+                 b_us = sizeof(int64_t) * n * 2, b_rec = sizeof(int32_t) * n * (kRec + 1);
+    char* work = nullptr;
+    AFM_HIP(hipMallocAsync((void**)&work, b_pb + b_up + b_us + b_rec, ctx->stream));
+    uint64_t* pbits = (uint64_t*)work;
+    int64_t* usize = (int64_t*)(work + b_pb);
+    int32_t* upos = (int32_t*)(work + b_pb + b_us);
+    int32_t* rec = (int32_t*)(work + b_pb + b_us + b_up);
+    int32_t* rlen = rec + n * kRec;
+    hipLaunchKernelGGL(pred_bits_kernel, dim3((unsigned)((nw + 3) / 4), (unsigned)nd), dim3(256),
+                       0, ctx->stream, lda, dates, nd, pred, pbits);
+    AFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(pair_union_kernel, dim3((unsigned)n), dim3(64), 0, ctx->stream, steps,
+                       path, nw, pbits, k_out, books, upos, usize);
+    AFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(turnover_terms_kernel, dim3((unsigned)n), dim3(64), 0, ctx->stream, n,
+                       k_out, books, upos, usize, rec, rlen, path, steps);
+    AFM_HIP(hipGetLastError());
+    hipLaunchKernelGGL(pnl_scan_kernel, dim3((unsigned)npaths), dim3(128), 0, ctx->stream, steps,
+                       sums, rec, rlen, v0, rate, value, turnover, long_ret, short_ret, path);
+    AFM_HIP(hipGetLastError());
+    AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;
 }

@@ -135,6 +135,18 @@ int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out, const int32
                      const double* sums, const int32_t* upos, const int64_t* usize, double v0,
                      double rate, double* value, double* turnover, double* long_ret,
                      double* short_ret);
+/* Bootstrap of the rebalance sequence (BASELINE config E): npaths paths of `steps` book slots
+ * each, path [npaths][steps] (DEVICE int32, slots into the nd dates of one afm_rebalance_f64
+ * call, drawn with replacement).  Every path re-runs the value / turnover recursion of
+ * afm_pnl_scan_f64 (KKT:864-892) over its steps, with the turnover aligned on the union of the
+ * previous and current step's prediction sets (pred [T][lda], dates as passed to
+ * afm_rebalance_f64).  value [npaths][steps+1], turnover / long_ret / short_ret
+ * [npaths][steps]. */
+int afm_bootstrap_pnl_f64(afm_ctx* ctx, int64_t lda, const int32_t* dates, int64_t nd,
+                          const double* pred, const int32_t* k_out, const int32_t* books,
+                          const double* sums, int64_t npaths, int64_t steps, const int32_t* path,
+                          double v0, double rate, double* value, double* turnover,
+                          double* long_ret, double* short_ret);
 /* determine_weights (KKT:817-833) for one book: R [rows][ld] returns (k columns, NaN = missing)
  * -> pairwise-complete covariance cov[k][k] and the exact box-QP weights w[k]. */
 int afm_min_variance_weights_f64(afm_ctx* ctx, const double* R, int64_t rows, int64_t ld, int k,

@@ -140,49 +140,49 @@ def book_history(hist_date, hist_id, hist_val, book, window: int | None = None, 
     return R
 
 
-def run_portfolio(pred_date, pred_id, pred, hist_date, hist_id, hist, all_date, all_id,
-                  all_tradable, all_close, all_tmr, trading_cost_rate=1e-4, top_n=10,
-                  window=None, lo=0.0, hi=0.1):
-    """PortfolioManager.calculate_portfolio (KKT:842-892) with the exact weight solve."""
-    V = [100000000.0]
-    turnovers, long_r, short_r, books, weights = [], [], [], [], []
-    cur = None                                   # (ids, positions) of the previous date
-    akey = {(d, i): j for j, (d, i) in enumerate(zip(all_date.tolist(), all_id.tolist()))}
-    udates = np.unique(pred_date)
-    calendar = np.unique(np.concatenate([pred_date, hist_date, all_date]))
-    for dt in udates:
-        m = pred_date == dt
-        ids, vals = pred_id[m], pred[m]
-        rows = np.array([akey.get((dt, i), -1) for i in ids.tolist()])
-        trad = np.array([r >= 0 and bool(all_tradable[r]) for r in rows])
-        L, S = select_books(ids, vals, trad, top_n)
-        wl = box_qp_weights(pairwise_cov(book_history(hist_date, hist_id, hist, L, window, dt,
-                                                      calendar)), lo, hi)[0]
-        ws = box_qp_weights(pairwise_cov(book_history(hist_date, hist_id, hist, S, window, dt,
-                                                      calendar)), lo, hi)[0]
-        books += [L, S]
-        weights += [wl, ws]
+def _date_books(dt, pred_date, pred_id, pred, hist_date, hist_id, hist, akey, all_tradable,
+                all_close, all_tmr, calendar, top_n, window, lo, hi):
+    """The path-independent part of one rebalance date (KKT:844-877): books, weights, PnL sums."""
+    m = pred_date == dt
+    ids, vals = pred_id[m], pred[m]
+    rows = np.array([akey.get((dt, i), -1) for i in ids.tolist()])
+    trad = np.array([r >= 0 and bool(all_tradable[r]) for r in rows])
+    L, S = select_books(ids, vals, trad, top_n)
+    wl = box_qp_weights(pairwise_cov(book_history(hist_date, hist_id, hist, L, window, dt,
+                                                  calendar)), lo, hi)[0]
+    ws = box_qp_weights(pairwise_cov(book_history(hist_date, hist_id, hist, S, window, dt,
+                                                  calendar)), lo, hi)[0]
+    rl = np.array([all_tmr[akey[(dt, i)]] for i in L.tolist()])
+    rs = np.array([all_tmr[akey[(dt, i)]] for i in S.tolist()])
+    pl = np.array([all_close[akey[(dt, i)]] for i in L.tolist()])
+    ps = np.array([all_close[akey[(dt, i)]] for i in S.tolist()])
+    lsum, ssum = np_sum(np.nan_to_num(rl * wl)), np_sum(np.nan_to_num(rs * ws))
+    den_l = 0
+    for x in (wl * pl).tolist():                 # builtin sum(): 0 + x0 + x1 ...
+        den_l = den_l + x
+    den_s = 0
+    for x in (ws * ps).tolist():
+        den_s = den_s + x
+    return dict(ids=ids, L=L, S=S, wl=wl, ws=ws, lsum=lsum, ssum=ssum, den_l=den_l, den_s=den_s)
+
+
+def _value_recursion(seq, trading_cost_rate, v0=100000000.0):
+    """KKT:864-892 over a sequence of per-date records (a date may repeat: bootstrap paths)."""
+    V = [v0]
+    turnovers, long_r, short_r = [], [], []
+    cur = None                                   # (ids, positions) of the previous step
+    for b in seq:
+        ids = b["ids"]
         size = V[-1] / 2
-        rl = np.array([all_tmr[akey[(dt, i)]] for i in L.tolist()])
-        rs = np.array([all_tmr[akey[(dt, i)]] for i in S.tolist()])
-        pl = np.array([all_close[akey[(dt, i)]] for i in L.tolist()])
-        ps = np.array([all_close[akey[(dt, i)]] for i in S.tolist()])
-        lsum, ssum = np_sum(np.nan_to_num(rl * wl)), np_sum(np.nan_to_num(rs * ws))
-        daily = (lsum - ssum) / 2
-        long_r.append(lsum)
-        short_r.append(ssum)
+        daily = (b["lsum"] - b["ssum"]) / 2
+        long_r.append(b["lsum"])
+        short_r.append(b["ssum"])
         newpos = np.full(len(ids), np.nan)
         idx = {x: j for j, x in enumerate(ids.tolist())}
-        den_l = 0
-        for x in (wl * pl).tolist():             # builtin sum(): 0 + x0 + x1 ...
-            den_l = den_l + x
-        den_s = 0
-        for x in (ws * ps).tolist():
-            den_s = den_s + x
-        for x in L.tolist():
-            newpos[idx[x]] = size / den_l
-        for x in S.tolist():
-            newpos[idx[x]] = -size / den_s
+        for x in b["L"].tolist():
+            newpos[idx[x]] = size / b["den_l"]
+        for x in b["S"].tolist():
+            newpos[idx[x]] = -size / b["den_s"]
         if cur is None or np.all(np.isnan(cur[1])):
             to = 0.0
         else:                                    # (cur.fillna(0) - new.fillna(0)) on the union
@@ -199,7 +199,43 @@ def run_portfolio(pred_date, pred_id, pred, hist_date, hist_id, hist, all_date, 
         V.append(V[-1] * (1 + daily))
         cur = (ids, newpos)
     return {"value": np.array(V), "turnover": np.array(turnovers), "long_ret": np.array(long_r),
-            "short_ret": np.array(short_r), "books": books, "weights": weights, "dates": udates}
+            "short_ret": np.array(short_r)}
+
+
+def _all_books(pred_date, pred_id, pred, hist_date, hist_id, hist, all_date, all_id,
+               all_tradable, all_close, all_tmr, top_n, window, lo, hi):
+    akey = {(d, i): j for j, (d, i) in enumerate(zip(all_date.tolist(), all_id.tolist()))}
+    udates = np.unique(pred_date)
+    calendar = np.unique(np.concatenate([pred_date, hist_date, all_date]))
+    recs = [_date_books(dt, pred_date, pred_id, pred, hist_date, hist_id, hist, akey,
+                        all_tradable, all_close, all_tmr, calendar, top_n, window, lo, hi)
+            for dt in udates]
+    return udates, recs
+
+
+def run_portfolio(pred_date, pred_id, pred, hist_date, hist_id, hist, all_date, all_id,
+                  all_tradable, all_close, all_tmr, trading_cost_rate=1e-4, top_n=10,
+                  window=None, lo=0.0, hi=0.1):
+    """PortfolioManager.calculate_portfolio (KKT:842-892) with the exact weight solve."""
+    udates, recs = _all_books(pred_date, pred_id, pred, hist_date, hist_id, hist, all_date,
+                              all_id, all_tradable, all_close, all_tmr, top_n, window, lo, hi)
+    res = _value_recursion(recs, trading_cost_rate)
+    res["books"] = [x for b in recs for x in (b["L"], b["S"])]
+    res["weights"] = [x for b in recs for x in (b["wl"], b["ws"])]
+    res["dates"] = udates
+    return res
+
+
+def run_bootstrap(paths, pred_date, pred_id, pred, hist_date, hist_id, hist, all_date, all_id,
+                  all_tradable, all_close, all_tmr, trading_cost_rate=1e-4, top_n=10,
+                  window=None, lo=0.0, hi=0.1):
+    """Bootstrap of the rebalance sequence (BASELINE config E): ``paths`` [npaths][steps] indices
+    into the sorted unique prediction dates; every path re-runs the KKT:864-892 recursion over
+    its steps (books per date are path-independent)."""
+    _, recs = _all_books(pred_date, pred_id, pred, hist_date, hist_id, hist, all_date, all_id,
+                         all_tradable, all_close, all_tmr, top_n, window, lo, hi)
+    out = [_value_recursion([recs[j] for j in row], trading_cost_rate) for row in np.asarray(paths)]
+    return {k: np.stack([o[k] for o in out]) for k in out[0]} if out else {}
 
 
 def sharpe(V):

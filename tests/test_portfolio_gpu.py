@@ -133,3 +133,54 @@ def test_tied_predictions_books_vs_oracle(A, levels):
                         d.astype(np.int64), i, trad, close, ret, top_n=top_n, window=60)
     for (dt, L, S), Lo, So in zip(pm.books, o["books"][0::2], o["books"][1::2]):
         assert L == Lo.tolist() and S == So.tolist()
+
+
+@pytest.mark.parametrize("top_n,window,npaths", [(10, 60, 37), (20, None, 8)])
+def test_bootstrap_paths_vs_oracle(top_n, window, npaths):
+    """Config E: bootstrap resamples of the rebalance dates (with replacement, repeated
+    consecutive dates included); every path's value / turnover recursion vs the oracle's
+    KKT:864-892 restatement over the same date sequence.  The identity path reproduces
+    calculate_portfolio.  top_n = 10 (weights exactly 0.1): bit-exact; top_n = 20 (active-set
+    QP weights, rel 1e-9 vs the oracle): the values at rel 1e-12."""
+    from afm.portfolio import PortfolioManager
+    from oracle import portfolio as P
+    rng = np.random.default_rng(100 + top_n)
+    T, A = 150, 70
+    dates = np.asarray(np.busday_offset(np.datetime64("2016-01-04"), np.arange(T), roll="forward"),
+                       dtype="datetime64[ns]")
+    ids = 300 + 5 * np.arange(A)
+    present = rng.random((T, A)) < 0.9
+    present[140, :] = False
+    present[140, :30] = True                                      # a thin date: k = n // 2
+    tt, aa = np.nonzero(present)
+    d, i = dates[tt], ids[aa]
+    ret = rng.normal(0, 0.02, len(tt))
+    close = 50 * np.exp(rng.normal(0, 0.1, len(tt)))
+    trad = rng.random(len(tt)) < 0.9
+    hist_m = tt < 100
+    test_m = tt >= 100
+    pred_v = rng.normal(size=test_m.sum())
+    pred = pd.DataFrame({"p": pred_v}, index=pd.MultiIndex.from_arrays([d[test_m], i[test_m]]))
+    hist = pd.DataFrame({"target": ret[hist_m]}, index=pd.MultiIndex.from_arrays([d[hist_m], i[hist_m]]))
+    all_df = pd.DataFrame({"in_trading_universe": np.where(trad, "Y", "N"), "close_price": close,
+                           "tmr_ret1d": ret}, index=pd.MultiIndex.from_arrays([d, i]))
+    pm = PortfolioManager(pred, hist, all_df, top_n=top_n, window=window)
+    nd = 50
+    paths = np.random.default_rng(2023).integers(0, nd, size=(npaths, nd)).astype(np.int32)
+    paths[1, 5:9] = 17                                            # repeated consecutive dates
+    paths[2] = np.arange(nd)                                      # the plain sequence
+    got_paths, got = pm.bootstrap(paths=paths)
+    assert (got_paths == paths).all()
+    o = P.run_bootstrap(paths, d[test_m].astype(np.int64), i[test_m], pred_v,
+                        d[hist_m].astype(np.int64), i[hist_m], ret[hist_m], d.astype(np.int64), i,
+                        trad, close, ret, top_n=top_n, window=window)
+    if top_n == 10:
+        for k in ("value", "turnover", "long_ret", "short_ret"):
+            assert same(got[k], o[k]), k
+    else:
+        assert np.abs(got["value"] - o["value"]).max() / o["value"].max() < 1e-12
+        assert np.abs(got["turnover"] - o["turnover"]).max() <= 1e-9 * max(1.0, o["turnover"].max())
+    pm.calculate_portfolio()
+    v = np.asarray(pm.portfolio_value["Portfolio"], dtype=np.float64)
+    assert same(got["value"][2], v)
+    assert same(got["turnover"][2, 1:], np.asarray(pm.turnovers[1:], dtype=np.float64))
