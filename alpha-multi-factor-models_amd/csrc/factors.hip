@@ -52,6 +52,9 @@ constexpr int kRing = AFM_FP_RING;     // experiments only
 #else
 constexpr int kRing = 57 + 2 * kChunk + 1;
 #endif
+#ifndef AFM_FP_WPE3
+#define AFM_FP_WPE3 3
+#endif
 constexpr int kJobSets = 15;      // job waves per 64-asset block (W0..W14 below)
 
 typedef unsigned long long u64;
@@ -127,6 +130,8 @@ struct Args {
     GLB uint64_t* badpart;     // [types][nch][lda] per-type "some output non-finite" bits
     int types;                 // workgroups per 64-asset block (1, 3, 5 or 15)
     int fast;                  // 0: general step only (A/B tests)
+    int nblk;                  // 64-asset blocks (paired launch: items = nblk * types)
+    int pslot;                 // profiling build: block * types + type of the running item
 };
 
 // Ring cell of lookback L (observation p - L) as a byte offset from row 0, given pmoff = the
@@ -840,6 +845,17 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
     }
 }
 
+// A wave with no item (odd item count in the paired launch): the loader's barrier sequence.
+__device__ __forceinline__ void idle_wave(const Args& a) {
+    const int nch = (int)((a.T + kChunk - 1) / kChunk);
+    lds_barrier();
+    for (int ch = 0; ch < nch; ++ch) {
+        const int sh = (ch * kChunk) & 63;
+        if (sh + kChunk == 64 || ch + 1 == nch) { lds_barrier(); lds_barrier(); }
+        lds_barrier();
+    }
+}
+
 template <class P>
 __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type, int wave, int lane,
                                       int64_t block) {
@@ -960,33 +976,58 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     if (lane == 0) {
         const long long tot = __builtin_readcyclecounter() - tstart;
         const int jw = kJobSets / a.types;
+        const int slot = a.pslot;
         const long long tend = (long long)__builtin_amdgcn_s_memrealtime();
-        g_wave_cycles[(blockIdx.x * jw + wave) * 4 % (1 << 16)] = tot;
-        g_wave_cycles[((blockIdx.x * jw + wave) * 4 + 1) % (1 << 16)] = twait;
-        g_wave_cycles[((blockIdx.x * jw + wave) * 4 + 2) % (1 << 16)] = treal;
-        g_wave_cycles[((blockIdx.x * jw + wave) * 4 + 3) % (1 << 16)] = tend;
+        g_wave_cycles[(slot * jw + wave) * 4 % (1 << 16)] = tot;
+        g_wave_cycles[((slot * jw + wave) * 4 + 1) % (1 << 16)] = twait;
+        g_wave_cycles[((slot * jw + wave) * 4 + 2) % (1 << 16)] = treal;
+        g_wave_cycles[((slot * jw + wave) * 4 + 3) % (1 << 16)] = tend;
     }
 #endif
 }
 
 // TYPES workgroups per block, each with J = 15 / TYPES job waves (job sets W[J*type + wave]) and
-// a loader wave.  Every workgroup needs its own 78-KB ring, so a CU holds at most two; TYPES = 1
-// (15 + 1 waves, 4 waves / SIMD, one per CU) only when even the 3-way split would not be
-// resident at once (10k assets: 157 blocks x 3 = 471 workgroups on 256 CUs, two per CU).
-template <int TYPES>
-__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1)) __attribute__((amdgpu_waves_per_eu(TYPES == 1 ? 4 : TYPES == 3 ? 3 : 2)))
+// a loader wave.  PAIR: one workgroup runs TWO such items (two rings, 2 x (J + 1) waves), items
+// ordered type-major so a pair shares its job sets.  At 10k assets the 3-way split has 471 items
+// of 6 waves and 78 KB of LDS; at 168 VGPRs (3 waves / SIMD) two separate 6-wave workgroups
+// rarely co-reside on a CU (their waves land 2-2-1-1 on the SIMDs), so half of them ran in a
+// second round; paired, 236 workgroups of 12 waves (3 per SIMD, 156 KB LDS) are all resident.
+// Paired 3-way launch: job (0-4) or loader (5) run at wave position k of each half, per type.
+// Wave w of a workgroup issues on SIMD w % 4; the layouts minimise the busiest SIMD's measured
+// cycles (tools/wave_profile.py; type 1: 61.3 -> 55.0 Mcycles).
+__constant__ const signed char kPairLayout[3][2][6] = {
+    {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
+    {{0, 2, 3, 4, 1, 5}, {1, 2, 3, 4, 0, 5}},
+    {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
+};
+
+template <int TYPES, bool PAIR>
+__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1) * (PAIR ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(TYPES == 1 ? 4 : TYPES == 3 ? AFM_FP_WPE3 : 2)))
 void factor_panel_kernel(Args a) {
     constexpr int J = kJobSets / TYPES;
     // dynamic LDS: with a static size the compiler pads the VGPR allocation of the split
-    // variants up to what it thinks the LDS occupancy allows, and two 6-wave workgroups then no
-    // longer fit one CU
+    // variants up to what it thinks the LDS occupancy allows
     extern __shared__ double sm_dyn[];
-    LDS Smem* sm = (LDS Smem*)sm_dyn;
     const int lane = threadIdx.x & (kLanes - 1);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int type = (int)(blockIdx.x % TYPES);
-    const int64_t block = blockIdx.x / TYPES;
-    if (threadIdx.x < 128) sm->rtab[threadIdx.x] = 1.0 / (double)threadIdx.x;
+    const int wall = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int half = PAIR ? (wall >= J + 1 ? 1 : 0) : 0;
+    const int pos = wall - half * (J + 1);
+    LDS Smem* sm = (LDS Smem*)sm_dyn + half;
+    int type;
+    int64_t block;
+    if (PAIR) {
+        const int64_t item = 2 * (int64_t)blockIdx.x + half;
+        if (item >= (int64_t)a.nblk * TYPES) { idle_wave(a); return; }
+        type = (int)(item / a.nblk);
+        block = item % a.nblk;
+    } else {
+        type = (int)(blockIdx.x % TYPES);
+        block = blockIdx.x / TYPES;
+    }
+    // job index of this wave (J = the loader)
+    const int wave = PAIR && TYPES == 3 ? (int)kPairLayout[type][half][pos] : pos;
+    const int ltid = (int)threadIdx.x - half * (J + 1) * kLanes;
+    if (ltid < 128) sm->rtab[ltid] = 1.0 / (double)ltid;
     // (the loader's first barrier also publishes rtab)
     if (wave == J) { load_wave(a, sm, lane, block); return; }
     // this type's partial-mask planes (keeps the type out of the job waves' registers)
@@ -994,6 +1035,13 @@ void factor_panel_kernel(Args a) {
     const int64_t po = (int64_t)type * ((a.T + 63) / 64) * a.lda;
     at.nanpart = a.nanpart + po;
     at.badpart = a.badpart + po;
+#ifdef AFM_FP_PROFILE
+    at.pslot = (int)(block * TYPES + type);          // profile slot of this item
+#endif
+#ifdef AFM_FP_ONLY
+    run_wave<AFM_FP_ONLY>(at, sm, 0, wave, lane, block);
+    return;
+#endif
     switch (type * J + wave) {
         case 0: run_wave<W0>(at, sm, 0, wave, lane, block); break;
         case 1: run_wave<W1>(at, sm, 0, wave, lane, block); break;
@@ -1116,32 +1164,46 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     a.nanpart = (GLB uint64_t*)part;
     a.badpart = (GLB uint64_t*)(part + types * nwords * lda);
     a.types = types;
+    a.nblk = (int)nblk;
+    a.pslot = 0;
     a.fast = 1;
+    // paired 12-wave workgroups for the 3-way split (see factor_panel_kernel); AFM_FP_PAIR=0: A/B
+    bool pair = true;
+    if (const char* e = getenv("AFM_FP_PAIR")) pair = atoi(e) != 0;
     if (const char* e = getenv("AFM_FP_NOFAST"))                   // A/B: general step only
         a.fast = atoi(e) ? 0 : 1;
     const dim3 grid((unsigned)(nblk * types));
     static bool lds_attr = false;                     // > 64 KB of dynamic LDS: opt in once
     if (!lds_attr) {
         const int bytes = (int)sizeof(afm::Smem);
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<1>,
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<1, false>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<3>,
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<3, false>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<5>,
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<3, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 2 * bytes));
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<5, false>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<15>,
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<15, false>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
         lds_attr = true;
     }
     switch (types) {
-        case 1: hipLaunchKernelGGL(afm::factor_panel_kernel<1>, grid, dim3(64 * 16), sizeof(afm::Smem),
-                                   ctx->stream, a); break;
-        case 3: hipLaunchKernelGGL(afm::factor_panel_kernel<3>, grid, dim3(64 * 6), sizeof(afm::Smem),
-                                   ctx->stream, a); break;
-        case 5: hipLaunchKernelGGL(afm::factor_panel_kernel<5>, grid, dim3(64 * 4), sizeof(afm::Smem),
-                                   ctx->stream, a); break;
-        default: hipLaunchKernelGGL(afm::factor_panel_kernel<15>, grid, dim3(64 * 2), sizeof(afm::Smem),
-                                    ctx->stream, a); break;
+        case 1: hipLaunchKernelGGL((afm::factor_panel_kernel<1, false>), grid, dim3(64 * 16),
+                                   sizeof(afm::Smem), ctx->stream, a); break;
+        case 3:
+            if (pair)
+                hipLaunchKernelGGL((afm::factor_panel_kernel<3, true>),
+                                   dim3((unsigned)((nblk * 3 + 1) / 2)), dim3(64 * 12),
+                                   2 * sizeof(afm::Smem), ctx->stream, a);
+            else
+                hipLaunchKernelGGL((afm::factor_panel_kernel<3, false>), grid, dim3(64 * 6),
+                                   sizeof(afm::Smem), ctx->stream, a);
+            break;
+        case 5: hipLaunchKernelGGL((afm::factor_panel_kernel<5, false>), grid, dim3(64 * 4),
+                                   sizeof(afm::Smem), ctx->stream, a); break;
+        default: hipLaunchKernelGGL((afm::factor_panel_kernel<15, false>), grid, dim3(64 * 2),
+                                    sizeof(afm::Smem), ctx->stream, a); break;
     }
     AFM_HIP(hipGetLastError());
     const int64_t nw = nwords * lda;

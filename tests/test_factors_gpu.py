@@ -57,16 +57,20 @@ def test_factor_grid_vs_oracle(A, T, seed, kw):
     assert np.array_equal(nf, exp)
 
 
-@pytest.mark.parametrize("types", ["1", "3", "5", "15"])
-def test_factor_workgroup_splits_identical(types, monkeypatch):
+@pytest.mark.parametrize("types,pair,A", [("1", "1", 200), ("3", "1", 200), ("3", "1", 300),
+                                          ("3", "0", 200), ("5", "1", 200), ("15", "1", 200)])
+def test_factor_workgroup_splits_identical(types, pair, A, monkeypatch):
     """Every split of a block's 15 job waves over 1, 3, 5 or 15 workgroups (chosen from the
-    shard's block count; AFM_FP_TYPES overrides) gives the same bit-exact panel and masks."""
+    shard's block count; AFM_FP_TYPES overrides), paired two items per workgroup or not
+    (AFM_FP_PAIR; A = 300 leaves the last pair half idle), gives the same bit-exact panel and
+    masks."""
     import torch
     import afm
     from afm.synthetic import make_panel
-    p = make_panel(200, 500, seed=9, edge_cases=True, hole_frac=0.01, listing_frac=0.2)
+    p = make_panel(A, 500, seed=9, edge_cases=True, hole_frac=0.01, listing_frac=0.2)
     grid = afm.PanelGrid.from_panel(p)
     monkeypatch.setenv("AFM_FP_TYPES", types)
+    monkeypatch.setenv("AFM_FP_PAIR", pair)
     fin = torch.zeros_like(grid.vbits)
     out, nanfree = afm.factor_panel(grid, finite=fin)
     torch.cuda.synchronize()
