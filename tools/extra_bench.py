@@ -6,7 +6,10 @@
 * bootstrap -- BASELINE config E: 1,024 bootstrap paths x 5,000 assets: rebalance (books,
                rolling-252 covariance, exact KKT weights) once per date, then every path's
                union alignment, turnover DAGs and value recursion.
-Usage: python tools/extra_bench.py [--only zscore|bootstrap] [--reps N]"""
+* intraday  -- BASELINE config D: 3,000 assets x 196,560 one-minute bars (2 years x 252 days x
+               390 bars), the 98-column factor build streamed over asset groups sized to HBM
+               (afm/intraday.py); algorithmic bytes 816 per present asset-bar.
+Usage: python tools/extra_bench.py [--only zscore|bootstrap|intraday] [--reps N]"""
 import argparse
 import json
 import os
@@ -79,12 +82,30 @@ def bench_bootstrap(reps, n_paths=1024, A=5000, T=5040):
             "path_steps_per_s": round(n_paths * nd / ((ms_boot) * 1e-3), 1)}
 
 
+def bench_intraday(reps, A=3000, T=2 * 252 * 390):
+    import torch
+    from afm.intraday import factor_panel_groups, group_blocks, make_panel_device
+    g = make_panel_device(A, T, seed=2023)
+    bars = int(g.valid.sum().item())
+    bpg = group_blocks(g)
+    groups = []
+    factor_panel_groups(g, lambda a0, a1, o, nf: groups.append((a0, a1)), bpg)   # warm-up
+    ms = timed(lambda: factor_panel_groups(g, lambda *x: None, bpg), max(1, reps // 3))
+    byts = 816 * bars
+    return {"stage": "intraday", "workload": f"config D: {A} assets x {T} 1-minute bars "
+                                             f"({bars} present asset-bars), 98 factors, "
+                                             f"{len(groups)} asset groups of {bpg} blocks",
+            "ms": round(ms, 1), "asset_bars_per_s": round(bars / (ms * 1e-3), 1),
+            "algorithmic_GB": round(byts / 1e9, 1), "GBps": round(byts / (ms * 1e-3) / 1e9, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
-    for nm, fn in (("zscore", bench_zscore), ("bootstrap", bench_bootstrap)):
+    for nm, fn in (("zscore", bench_zscore), ("bootstrap", bench_bootstrap),
+                   ("intraday", bench_intraday)):
         if a.only and a.only != nm:
             continue
         t0 = time.perf_counter()
