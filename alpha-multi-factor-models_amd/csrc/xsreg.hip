@@ -17,8 +17,19 @@
 //   fragments.  Waves: 2 pair groups x 2 row halves; partial sums are combined in a fixed order,
 //   so results are deterministic.  The shift is found in the first block holding a usable row;
 //   later blocks subtract it while staging.
+// Two passes (MI355X: f64 MFMA and VALU share the SIMD's f64 pipe -- tools/mfma_probe: a partner
+// wave's VALU instruction issues only between MFMAs -- so every producer VALU instruction costs
+// MFMA-pipe time): the FAST pass stages rows without the
+// per-row finiteness check; any masked-in non-finite value makes its column's diagonal entry
+// non-finite (d*d never returns to finite), so the REDO pass re-runs exactly those segments with
+// the checked staging (rows with a non-finite value excluded).  On segments with no such row
+// both stagings perform the same operations: results are identical to a checked-only run.
+// The FAST pass also drops the per-block barrier: an S-slot LDS ring with ready / freed counters
+// lets the producers run up to S blocks ahead (S = 3 at p = 96).
 // Algorithmic work per segment: rows * (p+2)(p+3) flops over 8(p+1) B per row.
 #include "afm_internal.h"
+
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -40,6 +51,9 @@ constexpr int kMaxF = kMaxTiles * 16;
 constexpr int kRS = 66;               // LDS tile row stride (doubles)
 constexpr int kRows = 64;             // rows staged per tile
 constexpr int kThreads = 256;
+#ifndef AFM_GRAM_PRIO
+#define AFM_GRAM_PRIO 1
+#endif
 
 struct GramArgs {
     const double* base;      // planes / columns
@@ -80,15 +94,17 @@ struct Group {
     static constexpr int TMAX = GRP == 0 ? (NQ > 0 ? PairTab<NT>().J[Q1 - 1] + 1 : 0) : NT;
 };
 
-template <int NT>
+template <int NT, int S = 2>
 struct GramSmem {
     static constexpr int NF = NT * 16;
     static constexpr int NP = NT * (NT + 1) / 2;
     static constexpr int TROWS = NF + 2;             // x rows (zero padded), y row NF, dump NF+1
     // the epilogue reuses the tiles for the second row half's partial sums
     static constexpr int RED = NP * 256 + (2 * NT + 3) * 64;
-    static_assert(2 * TROWS * kRS >= RED, "epilogue scratch must fit in the tiles");
-    double tile[2][TROWS][kRS];                      // double-buffered 64-row blocks
+    static_assert(S * TROWS * kRS >= RED, "epilogue scratch must fit in the tiles");
+    double tile[S][TROWS][kRS];                      // S-slot ring of 64-row blocks
+    int ready[S];                                    // FAST: producer stagings of the slot so far
+    int freed[S];                                    // FAST: consumer releases of the slot so far
     double shs[NF + 2];                              // shifts of the tile rows (dump row: 0)
     int rowbad[2][kRows];                            // == b: row of block b is masked in but non-finite
     int anybad[2];                                   // == b: block b has such a row
@@ -97,6 +113,14 @@ struct GramSmem {
     int found;
     int srow;                                        // the shift row (first usable row)
 };
+
+// ring depth of the FAST kernel: as many 64-row slots as fit in 160 KB of LDS (at most 4)
+template <int NT>
+constexpr int fast_slots() {
+    constexpr int slot = (NT * 16 + 2) * kRS * 8;
+    constexpr int n = (160 * 1024 - 4096) / slot;
+    return n > 4 ? 4 : (n < 2 ? 2 : n);
+}
 
 // border sums (x, x*y) of tiles [LO, HI): split between the pair groups so that their VALU work
 // balances (group 1 also owns sum y, sum y*y)
@@ -115,8 +139,8 @@ __device__ __forceinline__ void lds_barrier() {
 
 // One staged block for a consumer wave.  Rows the mask leaves out, and masked-in rows with a
 // non-finite value (zeroed by the producers' fix-up step), are zero in the tile.
-template <int NT, int GRP>
-__device__ __forceinline__ void gram_block(GramSmem<NT>& sm, const int buf, const int kh, const int fi, const int kk,
+template <int NT, int GRP, int S>
+__device__ __forceinline__ void gram_block(GramSmem<NT, S>& sm, const int buf, const int kh, const int fi, const int kk,
                                            d4 (&acc)[Group<NT, GRP>::NQA], double (&bs)[NT],
                                            double (&bc)[NT], double& sy, double& syy) {
     using G = Group<NT, GRP>;
@@ -160,6 +184,11 @@ __device__ __forceinline__ void gram_block(GramSmem<NT>& sm, const int buf, cons
     }
 }
 
+template <int NT, int GRP, int S>
+__device__ void gram_epilogue(const GramArgs& g, GramSmem<NT, S>& sm, const int kh, const int lane,
+                              d4 (&acc)[Group<NT, GRP>::NQA], double (&bs)[NT], double (&bc)[NT],
+                              double& sy, double& syy);
+
 // Consumer wave (MFMA): pair group GRP, row half kh = wave & 1.  Block b lives in tile[b & 1].
 template <int NT, int GRP>
 __device__ void gram_consume(const GramArgs& g, GramSmem<NT>& sm, const int wave, const int lane,
@@ -184,7 +213,7 @@ __device__ void gram_consume(const GramArgs& g, GramSmem<NT>& sm, const int wave
         const int buf = b & 1;
         if (__builtin_amdgcn_readfirstlane(sm.anybad[buf]) == b) lds_barrier();   // fix-up step
 #if !defined(AFM_GRAM_SKIP) || AFM_GRAM_SKIP != 1      // experiments: producers alone
-        gram_block<NT, GRP>(sm, buf, kh, fi, kk, acc, bs, bc, sy, syy);
+        gram_block<NT, GRP, 2>(sm, buf, kh, fi, kk, acc, bs, bc, sy, syy);
 #endif
         GPROF_BAR(twait);                            // tile[buf] free, block b+1 staged
     }
@@ -197,12 +226,23 @@ __device__ void gram_consume(const GramArgs& g, GramSmem<NT>& sm, const int wave
     (void)tstart;
     (void)twait;
 #endif
+    gram_epilogue<NT, GRP, 2>(g, sm, kh, lane, acc, bs, bc, sy, syy);
+}
 
-    // ---- epilogue: row half 1 parks its partials, row half 0 adds them (fixed order) ----
+// Row half 1 parks its partials in the (now idle) tiles, row half 0 adds them (fixed order) and
+// writes the segment's Gram.  Entered right after a barrier that every wave executes.
+template <int NT, int GRP, int S>
+__device__ void gram_epilogue(const GramArgs& g, GramSmem<NT, S>& sm, const int kh, const int lane,
+                              d4 (&acc)[Group<NT, GRP>::NQA], double (&bs)[NT], double (&bc)[NT],
+                              double& sy, double& syy) {
+    using G = Group<NT, GRP>;
+    using B = Border<NT, GRP>;
+    constexpr PairTab<NT> tab{};
+    const int p = g.p;
     const int p2 = p + 2;
     double* out = g.gram + (int64_t)blockIdx.x * p2 * p2;
     double* red = &sm.tile[0][0][0] + (GRP == 0 ? 0 : Group<NT, 0>::NQ * 256);
-    double* rb = &sm.tile[0][0][0] + GramSmem<NT>::NP * 256;       // border partials
+    double* rb = &sm.tile[0][0][0] + GramSmem<NT, S>::NP * 256;    // border partials
     if (kh == 1) {
 #pragma unroll
         for (int q = 0; q < G::NQ; ++q)
@@ -280,7 +320,7 @@ __device__ void gram_consume(const GramArgs& g, GramSmem<NT>& sm, const int wave
 // non-finite value is flagged (rowbad / anybad) through a NaN-propagating x*0 sum.  Only loads:
 // its prefetches are never held behind stores.  With f64 MFMA, every VALU instruction of either
 // wave of a SIMD is issue time the matrix pipe loses, so this loop is written for VALU count.
-template <int NT>
+template <int NT, bool FAST>
 __device__ void gram_produce(const GramArgs& g, GramSmem<NT>& sm, const int pw, const int lane,
                              const int nb, const int64_t rmax) {
     constexpr int NF = NT * 16;
@@ -335,16 +375,21 @@ __device__ void gram_produce(const GramArgs& g, GramSmem<NT>& sm, const int pw, 
 #endif
         const int buf = b & 1;
         double* tb = &sm.tile[buf][0][0] + lane;
-        double chk = 0.0;
+        if (FAST) {                                  // no check: anybad / rowbad stay -1
 #pragma unroll
-        for (int j = 0; j < KPER; ++j) {
-            const double d = pre[j] - shv[j];
-            chk = __builtin_fma(d, 0.0, chk);        // NaN iff some d is not finite
-            tb[lrow_of(j) * kRS] = d;
+            for (int j = 0; j < KPER; ++j) tb[lrow_of(j) * kRS] = pre[j] - shv[j];
+        } else {
+            double chk = 0.0;
+#pragma unroll
+            for (int j = 0; j < KPER; ++j) {
+                const double d = pre[j] - shv[j];
+                chk = __builtin_fma(d, 0.0, chk);    // NaN iff some d is not finite
+                tb[lrow_of(j) * kRS] = d;
+            }
+            const bool bad = !(chk == 0.0);
+            if (bad) sm.rowbad[buf][lane] = b;                      // benign race: same value
+            if (__ballot(bad) != 0ull && lane == 0) sm.anybad[buf] = b;
         }
-        const bool bad = !(chk == 0.0);
-        if (bad) sm.rowbad[buf][lane] = b;                          // benign race: same value
-        if (__ballot(bad) != 0ull && lane == 0) sm.anybad[buf] = b;
         if (pw == 0) {
             // block b-1 is complete (a barrier separates the two stagings): count its rows
             if (okp && sm.rowbad[buf ^ 1][lane] != b - 1) ++cnt;
@@ -363,9 +408,6 @@ __device__ void gram_produce(const GramArgs& g, GramSmem<NT>& sm, const int pw, 
         }
         lds_barrier();
     };
-#ifndef AFM_GRAM_PRIO
-#define AFM_GRAM_PRIO 1
-#endif
     // the producers are the younger half: without priority they lose every VALU arbitration to
     // the MFMA waves of their SIMD (MI355X_MICROARCH.md, two waves per SIMD, item 4)
     if (AFM_GRAM_PRIO) __builtin_amdgcn_s_setprio(AFM_GRAM_PRIO);
@@ -423,19 +465,148 @@ __device__ void gram_produce(const GramArgs& g, GramSmem<NT>& sm, const int pw, 
     lds_barrier();                                   // the consumers' epilogue barrier
 }
 
+// ---- FAST pass: producers and consumers decoupled through an S-slot ring ------------------
+// Lock-step barriers made every block cost max(producer, consumer) plus the skew of both (the
+// producers' VALU issues only between the MFMAs of their SIMD partner, so their pace varies).
+// Here block b lives in slot b % S; ready[slot] counts producer stagings, freed[slot] consumer
+// releases (monotonic, one LDS atomic per wave and block).  Producers run up to S blocks ahead.
+__device__ __forceinline__ int lds_load_relaxed(int* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wait_count(int* p, int target) {
+    while (__builtin_amdgcn_readfirstlane(lds_load_relaxed(p)) < target)
+        __builtin_amdgcn_s_sleep(1);
+}
+// signal after every LDS access of this wave so far has completed
+__device__ __forceinline__ void signal_count(int* p, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int NT, int GRP, int S>
+__device__ void gram_consume_fast(const GramArgs& g, GramSmem<NT, S>& sm, const int wave,
+                                  const int lane, const int nb) {
+    using G = Group<NT, GRP>;
+    const int kh = wave & 1;
+    d4 acc[G::NQA];
+#pragma unroll
+    for (int q = 0; q < G::NQA; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+    double bs[NT], bc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { bs[t] = 0.0; bc[t] = 0.0; }
+    double sy = 0.0, syy = 0.0;
+    const int fi = lane & 15, kk = lane >> 4;
+    int slot = 0, gen = 1;
+    for (int b = 0; b < nb; ++b) {
+        wait_count(&sm.ready[slot], 4 * gen);
+        gram_block<NT, GRP, S>(sm, slot, kh, fi, kk, acc, bs, bc, sy, syy);
+        signal_count(&sm.freed[slot], lane);
+        if (++slot == S) { slot = 0; ++gen; }
+    }
+    lds_barrier();                                   // every wave is done with the ring
+    gram_epilogue<NT, GRP, S>(g, sm, kh, lane, acc, bs, bc, sy, syy);
+}
+
+template <int NT, int S>
+__device__ void gram_produce_fast(const GramArgs& g, GramSmem<NT, S>& sm, const int pw,
+                                  const int lane, const int nb, const int64_t rmax) {
+    constexpr int NF = NT * 16;
+    constexpr int KPER = (NF + 4) / 4;
+    const int64_t seg = g.seg0 + blockIdx.x;
+    const int p = g.p;
+    const double* src[KPER];
+    double shv[KPER];
+    auto lrow_of = [&](int j) {
+        const int f = pw + 4 * j;
+        return f < p ? f : (f == p ? NF : NF + 1);
+    };
+#pragma unroll
+    for (int j = 0; j < KPER; ++j) {
+        const int64_t o = sm.coff[pw + 4 * j];
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uint64_t)o);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uint64_t)o >> 32));
+        src[j] = g.base + (int64_t)(((uint64_t)hi << 32) | lo);
+        shv[j] = sm.shs[lrow_of(j)];
+    }
+    const uint64_t* bits = g.bits ? g.bits + (seg >> 6) * g.seg_stride : nullptr;
+    const int sb = (int)(seg & 63);
+    const unsigned srow = (unsigned)sm.srow;
+    auto bits_load = [&](int b) -> uint64_t {
+        if (!bits) return ~0ull;
+        int64_t r = (int64_t)b * kRows + lane;
+        r = r < rmax ? r : rmax;
+        return bits[r];
+    };
+    double pre0[KPER], pre1[KPER];
+    bool ok0 = false, ok1 = false;
+    int cnt = 0;                                     // producer 0: usable rows of this lane
+    auto load = [&](int b, double (&pre)[KPER], bool& ok, const uint64_t bw) {
+        const int64_t r = (int64_t)b * kRows + lane;
+        ok = r <= rmax && ((bw >> sb) & 1ull);
+        const unsigned off = (ok ? (unsigned)r : srow) * 8u;
+#pragma unroll
+        for (int j = 0; j < KPER; ++j)
+            pre[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(src[j]) + off);
+    };
+    int slot = 0, gen = 0;
+    auto stage = [&](const double (&pre)[KPER], const bool ok) {
+        wait_count(&sm.freed[slot], 4 * gen);        // the slot's previous block is consumed
+        double* tb = &sm.tile[slot][0][0] + lane;
+#pragma unroll
+        for (int j = 0; j < KPER; ++j) tb[lrow_of(j) * kRS] = pre[j] - shv[j];
+        if (pw == 0) cnt += ok ? 1 : 0;
+        signal_count(&sm.ready[slot], lane);
+        if (++slot == S) { slot = 0; ++gen; }
+    };
+    __builtin_amdgcn_s_setprio(AFM_GRAM_PRIO);
+    uint64_t bwA = bits_load(0), bwB = bits_load(1);
+    load(0, pre0, ok0, bwA);
+    bwA = bits_load(2);
+    if (nb > 1) {
+        load(1, pre1, ok1, bwB);
+        bwB = bits_load(3);
+    }
+    for (int b = 0; b < nb; b += 2) {
+        stage(pre0, ok0);
+        if (b + 2 < nb) {
+            load(b + 2, pre0, ok0, bwA);
+            bwA = bits_load(b + 4);
+        }
+        if (b + 1 >= nb) break;
+        stage(pre1, ok1);
+        if (b + 3 < nb) {
+            load(b + 3, pre1, ok1, bwB);
+            bwB = bits_load(b + 5);
+        }
+    }
+    if (pw == 0) sm.cnt[lane] = cnt;
+    lds_barrier();                                   // the consumers' ring-done barrier
+    lds_barrier();                                   // the consumers' epilogue barrier
+}
+
 // One workgroup per segment: 4 consumer waves (2 pair groups x 2 row halves) + 4 producer
 // waves; blocks of 64 rows double-buffered in LDS, one barrier per block.
-template <int NT>
+// MODE 0: checked staging; 1: FAST pass; 2: REDO pass (checked, only segments whose FAST result
+// has a non-finite diagonal entry -- the others exit at once).
+template <int NT, int MODE>
 __global__ __launch_bounds__(512, 1) void gram_kernel(GramArgs g) {
     constexpr int NF = NT * 16;
-    constexpr int TROWS = GramSmem<NT>::TROWS;
-    __shared__ GramSmem<NT> sm;
+    constexpr int S = MODE == 1 ? fast_slots<NT>() : 2;
+    constexpr int TROWS = GramSmem<NT, S>::TROWS;
+    __shared__ GramSmem<NT, S> sm;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int p = g.p, p2 = p + 2;
     const int64_t seg = g.seg0 + blockIdx.x;
     const int64_t rowbase = seg * g.seg_stride;
-    for (int i = tid; i < 2 * TROWS * kRS; i += 512) (&sm.tile[0][0][0])[i] = 0.0;
+    if (MODE == 2) {
+        const double* G = g.gram + (int64_t)blockIdx.x * p2 * p2;
+        bool bad = false;
+        for (int f = 1 + tid; f < p2; f += 512) bad = bad || !__builtin_isfinite(G[f * p2 + f]);
+        if (!__syncthreads_or(bad)) return;
+    }
+    for (int i = tid; i < S * TROWS * kRS; i += 512) (&sm.tile[0][0][0])[i] = 0.0;
+    if (tid < S) { sm.ready[tid] = 0; sm.freed[tid] = 0; }
     for (int i = tid; i < NF + 4; i += 512) {
         if (i <= NF + 1) sm.shs[i] = 0.0;
         const int c = i < p ? g.cols[i] : g.ycol;
@@ -481,9 +652,15 @@ __global__ __launch_bounds__(512, 1) void gram_kernel(GramArgs g) {
         return;
     }
     const int nb = (int)((rmax + kRows) / kRows);
-    if (wave < 2) gram_consume<NT, 0>(g, sm, wave, lane, nb);
-    else if (wave < 4) gram_consume<NT, 1>(g, sm, wave, lane, nb);
-    else gram_produce<NT>(g, sm, wave - 4, lane, nb, rmax);
+    if constexpr (MODE == 1) {
+        if (wave < 2) gram_consume_fast<NT, 0, S>(g, sm, wave, lane, nb);
+        else if (wave < 4) gram_consume_fast<NT, 1, S>(g, sm, wave, lane, nb);
+        else gram_produce_fast<NT, S>(g, sm, wave - 4, lane, nb, rmax);
+    } else {
+        if (wave < 2) gram_consume<NT, 0>(g, sm, wave, lane, nb);
+        else if (wave < 4) gram_consume<NT, 1>(g, sm, wave, lane, nb);
+        else gram_produce<NT, false>(g, sm, wave - 4, lane, nb, rmax);
+    }
     if (tid < p2) {
         const double v = tid == 0 ? 0.0 : (tid <= p ? sm.shs[tid - 1] : sm.shs[NF]);
         g.shift[(int64_t)blockIdx.x * p2 + tid] = v;
@@ -788,6 +965,29 @@ extern "C" int afm_debug_gram_cycles(long long* host, int n) {
 }
 #endif
 
+template <int NT>
+static hipError_t launch_gram_nt(int mode, dim3 grid, hipStream_t st, const GramArgs& g) {
+    const dim3 blk(512);
+    switch (mode) {
+        case 0: hipLaunchKernelGGL((gram_kernel<NT, 0>), grid, blk, 0, st, g); break;
+        case 1: hipLaunchKernelGGL((gram_kernel<NT, 1>), grid, blk, 0, st, g); break;
+        default: hipLaunchKernelGGL((gram_kernel<NT, 2>), grid, blk, 0, st, g); break;
+    }
+    return hipGetLastError();
+}
+
+static hipError_t launch_gram(int nt, int mode, dim3 grid, hipStream_t st, const GramArgs& g) {
+    switch (nt) {
+        case 1: return launch_gram_nt<1>(mode, grid, st, g);
+        case 2: return launch_gram_nt<2>(mode, grid, st, g);
+        case 3: return launch_gram_nt<3>(mode, grid, st, g);
+        case 4: return launch_gram_nt<4>(mode, grid, st, g);
+        case 5: return launch_gram_nt<5>(mode, grid, st, g);
+        case 6: return launch_gram_nt<6>(mode, grid, st, g);
+        default: return launch_gram_nt<7>(mode, grid, st, g);
+    }
+}
+
 extern "C" int afm_xs_gram_f64(afm_ctx* ctx, const double* base, int64_t col_stride,
                                int64_t seg_stride, int64_t seg_rows, int64_t row_limit,
                                const int32_t* cols, int p, int ycol, const uint64_t* bits,
@@ -801,17 +1001,13 @@ extern "C" int afm_xs_gram_f64(afm_ctx* ctx, const double* base, int64_t col_str
     GramArgs g{base, col_stride, seg_stride, seg_rows, row_limit, cols, ycol, p, bits, seg0, gram,
                shift};
     const int nt = (p + 15) / 16;
-    const dim3 grid((unsigned)nseg), blk(512);
-    switch (nt) {
-        case 1: hipLaunchKernelGGL((gram_kernel<1>), grid, blk, 0, ctx->stream, g); break;
-        case 2: hipLaunchKernelGGL((gram_kernel<2>), grid, blk, 0, ctx->stream, g); break;
-        case 3: hipLaunchKernelGGL((gram_kernel<3>), grid, blk, 0, ctx->stream, g); break;
-        case 4: hipLaunchKernelGGL((gram_kernel<4>), grid, blk, 0, ctx->stream, g); break;
-        case 5: hipLaunchKernelGGL((gram_kernel<5>), grid, blk, 0, ctx->stream, g); break;
-        case 6: hipLaunchKernelGGL((gram_kernel<6>), grid, blk, 0, ctx->stream, g); break;
-        default: hipLaunchKernelGGL((gram_kernel<7>), grid, blk, 0, ctx->stream, g); break;
+    // AFM_GRAM_CHECKED=1: the checked staging only (A/B tests)
+    const char* ce = getenv("AFM_GRAM_CHECKED");
+    const bool checked = ce && atoi(ce) != 0;
+    for (const int mode : {checked ? 0 : 1, checked ? -1 : 2}) {
+        if (mode < 0) break;
+        AFM_HIP(launch_gram(nt, mode, dim3((unsigned)nseg), ctx->stream, g));
     }
-    AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
 

@@ -48,6 +48,38 @@ def test_gram_long_mode_vs_numpy(p, n):
         assert np.abs(C[s] - ref).max() / scale.max() < 1e-12
 
 
+@pytest.mark.parametrize("mode", ["grid", "long"])
+def test_gram_fast_pass_identical_to_checked(mode, monkeypatch):
+    """FAST staging + REDO of segments with a non-finite diagonal == checked staging, bit for bit
+    (segments with masked-in non-finite rows in both x and y, and clean segments)."""
+    import torch
+    from afm.grid import pack_bits
+    from afm.regression import xs_gram
+    rng = np.random.default_rng(9)
+    p, T, lda = 40, 24, 640
+    Z = torch.from_numpy(rng.normal(size=(p + 1, T, lda)) * 3 + 20).cuda()
+    Z[3, 2, 17] = float("inf")
+    Z[p, 5, 100] = float("nan")                      # y
+    Z[7, 9, 0] = float("nan")                        # the would-be shift row
+    Z[0, 11, 33:40] = float("-inf")
+    valid = torch.from_numpy(rng.random((T, lda)) < 0.9).cuda()
+    bits = pack_bits(valid)
+    if mode == "grid":
+        args = (Z, T * lda, lda, lda, list(range(p)), p)
+        kw = dict(bits=bits, nseg=T)
+    else:
+        flat = Z.reshape(p + 1, T * lda)
+        args = (flat, T * lda, 500, 500, list(range(p)), p)
+        kw = dict(nseg=(T * lda + 499) // 500, row_limit=T * lda - 77)
+    g1, s1 = xs_gram(*args, **kw)
+    monkeypatch.setenv("AFM_GRAM_CHECKED", "1")
+    g0, s0 = xs_gram(*args, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(s0, s1)
+    assert torch.equal(g0, g1)
+    assert torch.isfinite(g0).all()
+
+
 def _panel_rows(seed=3, A=200, T=400):
     from afm.synthetic import make_panel
     p = make_panel(A, T, seed=seed, hole_frac=0.003)
