@@ -38,6 +38,7 @@ SIGNATURES = {
     "afm_ols_residual_f64": (I32, [P, P, I64, I32, I32, P, P, P]),
     "afm_vec_add_f64": (I32, [P, I64, P, P]),
     "afm_ols_intercept_f64": (I32, [P, I32, P, P]),
+    "afm_lasso_cd_f64": (I32, [P, P, I32, DBL, DBL, I32, DBL, I32, P, P]),
     "afm_rebalance_f64": (I32, [P, I64, I64, I64, P, I64, P, P, P, P, I64, I64, I64, P, P, I32,
                                 DBL, DBL, P, P, P, P, P, P, P]),
     "afm_pnl_scan_f64": (I32, [P, I64, P, P, P, P, P, DBL, DBL, P, P, P, P]),

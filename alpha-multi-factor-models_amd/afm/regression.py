@@ -211,3 +211,102 @@ class LinearRegression:
         out = predict_grid(base.view(p, 1, lda), lda, list(range(p)), self._beta, bits, 0, 1)
         pred = out[0, :n].cpu().numpy()
         return pred.reshape(-1, 1) if self._y2d else pred
+
+
+class ConvergenceWarning(UserWarning):
+    """Coordinate descent stopped at max_iter with the duality gap above tolerance (the
+    condition under which scikit-learn warns)."""
+
+
+class Lasso:
+    """Drop-in for ``sklearn.linear_model.Lasso`` as the reference uses it
+    (``Lasso(alpha=2e-4, max_iter=10000).fit(X_trainvalid, y_trainvalid)``, KKT:605-607).
+
+    Minimises ``(1 / (2 n)) ||y - X w - b||^2 + alpha ||w||_1``.  The design's centered moments
+    come from the same device Gram + Chan pooling as ``LinearRegression``; the fit is cyclic
+    coordinate descent on them (``afm_lasso_cd_f64``: sklearn's Gram coordinate descent with
+    its stopping rule and duality gap).  Results: ``coef_`` (p,), ``intercept_`` (float, or a
+    1-element array for a one-column DataFrame / 2-D y, as sklearn), ``n_iter_``,
+    ``dual_gap_`` (gap / n), ``n_features_in_``, ``feature_names_in_``."""
+
+    def __init__(self, alpha: float = 1.0, *, fit_intercept: bool = True, precompute=False,
+                 copy_X: bool = True, max_iter: int = 1000, tol: float = 1e-4,
+                 warm_start: bool = False, positive: bool = False, random_state=None,
+                 selection: str = "cyclic"):
+        if not fit_intercept:
+            raise NotImplementedError("only fit_intercept=True (the reference's usage)")
+        if selection != "cyclic":
+            raise NotImplementedError("only selection='cyclic' (the reference's usage)")
+        if warm_start:
+            raise NotImplementedError("warm_start is not supported")
+        if alpha < 0 or tol < 0 or max_iter < 1:
+            raise ValueError("alpha and tol must be >= 0 and max_iter >= 1")
+        self.alpha = float(alpha)
+        self.fit_intercept = True
+        self.precompute = precompute
+        self.copy_X = copy_X
+        self.max_iter = int(max_iter)
+        self.tol = float(tol)
+        self.warm_start = False
+        self.positive = bool(positive)
+        self.random_state = random_state
+        self.selection = selection
+
+    def fit(self, X, y):
+        import warnings
+
+        import torch
+        Xc, n, p, names = LinearRegression._as_columns(X)
+        yv = y.to_numpy(dtype=np.float64) if hasattr(y, "to_numpy") else y
+        y2d = getattr(yv, "ndim", 1) == 2
+        yt = torch.as_tensor(np.asarray(yv, dtype=np.float64) if not isinstance(yv, torch.Tensor)
+                             else yv, dtype=torch.float64).to(_dev()).reshape(-1)
+        if yt.numel() != n:
+            raise ValueError(f"X has {n} rows, y has {yt.numel()}")
+        if not (torch.isfinite(Xc).all() and torch.isfinite(yt).all()):
+            raise ValueError("Input contains NaN or infinity (as scikit-learn rejects it)")
+        if self.alpha == 0:
+            warnings.warn("With alpha=0 this is ordinary least squares by coordinate descent; "
+                          "LinearRegression is the better tool.", UserWarning)
+        Z = torch.cat([Xc, yt.view(1, -1)], dim=0).contiguous()
+        nseg = (n + SEG_ROWS - 1) // SEG_ROWS
+        gram, shift = xs_gram(Z, n, SEG_ROWS, SEG_ROWS, list(range(p)), p, nseg=nseg,
+                              row_limit=n)
+        g, s = pool_moments(gram, shift, p)
+        w = torch.empty(p, dtype=torch.float64, device=Z.device)
+        info = torch.empty(3, dtype=torch.float64, device=Z.device)
+        h = _lib.Context.get(Z.device.index).bind_stream()
+        _lib.check(_lib.lib().afm_lasso_cd_f64(h, _lib.ptr(g), p, self.alpha * n, 0.0,
+                                               self.max_iter, self.tol, int(self.positive),
+                                               _lib.ptr(w), _lib.ptr(info)), "afm_lasso_cd_f64")
+        G = g[0].cpu().numpy()
+        mean = s[0].cpu().numpy()[1:] + G[0, 1:] / G[0, 0]
+        gap, tol_y, n_iter = info.cpu().numpy()
+        self.coef_ = w.cpu().numpy()
+        x_off, y_off = mean[:p], mean[p]
+        icpt = y_off - np.dot(x_off, self.coef_)                 # sklearn _set_intercept
+        self.intercept_ = np.array([icpt]) if y2d else float(icpt)
+        self.n_iter_ = int(n_iter)
+        self.dual_gap_ = float(gap) / n
+        self.n_features_in_ = p
+        if names is not None:
+            self.feature_names_in_ = names
+        if self.n_iter_ >= self.max_iter and not gap < tol_y:
+            warnings.warn(f"Objective did not converge. Duality gap: {gap:.3e}, tolerance: "
+                          f"{tol_y:.3e}", ConvergenceWarning)
+        b = np.concatenate([[icpt], self.coef_])
+        self._beta = torch.from_numpy(b).to(Z.device)
+        return self
+
+    def predict(self, X):
+        import torch
+        Xc, n, p, _ = LinearRegression._as_columns(X)
+        if p != self.n_features_in_:
+            raise ValueError(f"X has {p} features, model was fit with {self.n_features_in_}")
+        lda = (n + 63) // 64 * 64
+        base = torch.zeros((p, lda), dtype=torch.float64, device=Xc.device)
+        base[:, :n] = Xc
+        bits = torch.zeros((1, lda), dtype=torch.int64, device=Xc.device)
+        bits[0, :n] = 1
+        out = predict_grid(base.view(p, 1, lda), lda, list(range(p)), self._beta, bits, 0, 1)
+        return out[0, :n].cpu().numpy()

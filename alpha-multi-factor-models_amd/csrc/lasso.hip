@@ -1,0 +1,147 @@
+// Lasso on the pooled Gram: the reference fits
+// sklearn Lasso(alpha=2e-4, max_iter=10000) on the pooled train+valid design
+// (KKT Yuliang Jiang.py:605-607).  The design's centered moments already exist on the device:
+// the per-segment shifted Grams (xsreg.hip gram_kernel) combined by pool_kernel.  So the fit is
+// cyclic coordinate descent on the centered Gram -- sklearn's enet_coordinate_descent_gram
+// (linear_model/_cd_fast.pyx, sklearn 1.7.2): H = Q w maintained by two axpys per coordinate,
+// soft-threshold update, stopping rule w_max == 0 or d_w_max / w_max < tol (or the last
+// iteration) followed by the duality gap test gap < tol * y'y.  Same operation order as
+// oracle/lasso_oracle.c (axpy = one fma per element, reductions sequential in feature order).
+//
+// One wave: lane j owns features j and j + 64 (p <= 110); H, w and q live in registers; the Gram
+// Q sits in LDS (a row per coordinate, conflict-free); the scalar step of a coordinate is
+// computed redundantly by every lane from readlane broadcasts.  The work is a few hundred
+// flops per coordinate on a dependency chain: latency-bound by construction (one date-free
+// solve per fit, ~microseconds per sweep over 96 coordinates).
+#include "afm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace afm {
+namespace {
+
+constexpr int kMaxLassoP = 110;
+
+__device__ __forceinline__ double bcast(double v, int lane) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, lane);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// value of feature j from the (v0: j < 64, v1: j >= 64) register pair, j uniform
+__device__ __forceinline__ double pick(double v0, double v1, int j) {
+    return j < 64 ? bcast(v0, j) : bcast(v1, j - 64);
+}
+__device__ __forceinline__ double fsign(double f) { return f == 0.0 ? 0.0 : (f > 0.0 ? 1.0 : -1.0); }
+
+__global__ __launch_bounds__(64) void lasso_cd_kernel(const double* gram, int p, double alpha,
+                                                      double beta, int max_iter, double tol,
+                                                      int positive, double* w_out, double* info) {
+    extern __shared__ double Q[];                    // [p][p] centered X'X
+    const int lane = threadIdx.x;
+    const int p2 = p + 2;
+    const double n = gram[0];
+    // centered moments C = G'[1:,1:] - (g0 g0^T) / n of [x, y] (oracle.centered_moments)
+    for (int e = lane; e < p * p; e += 64) {
+        const int i = e / p, j = e - i * p;
+        Q[e] = gram[(1 + i) * p2 + 1 + j] - (gram[1 + i] * gram[1 + j]) / n;
+    }
+    const int j0 = lane, j1 = lane + 64;
+    const bool has0 = j0 < p, has1 = j1 < p;
+    double q0 = 0.0, q1 = 0.0;
+    if (has0) q0 = gram[(1 + j0) * p2 + 1 + p] - (gram[1 + j0] * gram[1 + p]) / n;
+    if (has1) q1 = gram[(1 + j1) * p2 + 1 + p] - (gram[1 + j1] * gram[1 + p]) / n;
+    const double ynorm2 = gram[(1 + p) * p2 + 1 + p] - (gram[1 + p] * gram[1 + p]) / n;
+    __syncthreads();
+
+    double h0 = 0.0, h1 = 0.0, w0 = 0.0, w1 = 0.0;  // H = Q w, w (start at 0: H = 0)
+    double gap = tol + 1.0;
+    const double d_w_tol = tol;
+    const double tol_y = tol * ynorm2;
+    int n_iter = 0;
+    for (n_iter = 0; n_iter < max_iter; ++n_iter) {
+        double w_max = 0.0, d_w_max = 0.0;
+        for (int ii = 0; ii < p; ++ii) {
+            const double* row = Q + ii * p;
+            const double qii = row[ii];
+            if (qii == 0.0) continue;
+            const double r0 = has0 ? row[j0] : 0.0, r1 = has1 ? row[j1] : 0.0;
+            const double w_ii = pick(w0, w1, ii);
+            if (w_ii != 0.0) {
+                h0 = __builtin_fma(-w_ii, r0, h0);
+                h1 = __builtin_fma(-w_ii, r1, h1);
+            }
+            const double tmp = pick(q0, q1, ii) - pick(h0, h1, ii);
+            double wn;
+            if (positive && tmp < 0) wn = 0.0;
+            else wn = fsign(tmp) * __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0) / (qii + beta);
+            if (ii < 64) { if (lane == ii) w0 = wn; }
+            else if (lane == ii - 64) w1 = wn;
+            if (wn != 0.0) {
+                h0 = __builtin_fma(wn, r0, h0);
+                h1 = __builtin_fma(wn, r1, h1);
+            }
+            const double d_w_ii = __builtin_fabs(wn - w_ii);
+            if (d_w_ii > d_w_max) d_w_max = d_w_ii;
+            if (__builtin_fabs(wn) > w_max) w_max = __builtin_fabs(wn);
+        }
+        if (w_max == 0.0 || d_w_max / w_max < d_w_tol || n_iter == max_iter - 1) {
+            double q_dot_w = 0.0, wh = 0.0, w_norm2 = 0.0, asum = 0.0, dual = 0.0;
+            for (int j = 0; j < p; ++j) {
+                const double wj = pick(w0, w1, j), qj = pick(q0, q1, j), hj = pick(h0, h1, j);
+                q_dot_w = q_dot_w + wj * qj;
+                const double xta = qj - hj - beta * wj;
+                const double a = positive ? xta : __builtin_fabs(xta);
+                if (j == 0 || a > dual) dual = a;
+                wh = wh + wj * hj;
+                w_norm2 = w_norm2 + wj * wj;
+                asum = asum + __builtin_fabs(wj);
+            }
+            const double r_norm2 = ynorm2 + wh - 2.0 * q_dot_w;
+            double cst;
+            if (dual > alpha) {
+                cst = alpha / dual;
+                const double a_norm2 = r_norm2 * (cst * cst);
+                gap = 0.5 * (r_norm2 + a_norm2);
+            } else {
+                cst = 1.0;
+                gap = r_norm2;
+            }
+            gap = gap + (alpha * asum - cst * ynorm2 + cst * q_dot_w +
+                         0.5 * beta * (1 + cst * cst) * w_norm2);
+            if (gap < tol_y) break;
+        }
+    }
+    if (has0) w_out[j0] = w0;
+    if (has1) w_out[j1] = w1;
+    if (lane == 0) {
+        info[0] = gap;
+        info[1] = tol_y;
+        info[2] = (double)(n_iter < max_iter ? n_iter + 1 : max_iter);
+    }
+}
+
+}  // namespace
+}  // namespace afm
+
+extern "C" int afm_lasso_cd_f64(afm_ctx* ctx, const double* gram, int p, double alpha_n,
+                                double beta, int max_iter, double tol, int positive, double* w,
+                                double* info) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(p >= 1 && p <= afm::kMaxLassoP, "need 1 <= p <= 110");
+    AFM_CHECK_ARG(gram && w && info, "null buffer");
+    AFM_CHECK_ARG(max_iter >= 1, "max_iter must be >= 1");
+    AFM_CHECK_ARG(alpha_n >= 0 && beta >= 0 && tol >= 0, "alpha, beta and tol must be >= 0");
+    const int lds = (int)sizeof(double) * p * p;
+    static bool attr = false;
+    if (!attr) {
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::lasso_cd_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
+        attr = true;
+    }
+    hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(64), lds, ctx->stream, gram, p,
+                       alpha_n, beta, max_iter, tol, positive, w, info);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}

@@ -108,6 +108,15 @@ int afm_ols_intercept_f64(afm_ctx* ctx, int p, const double* mean, double* beta)
 /* Fama-MacBeth over segments with rank > 0: mean_t beta_t and mean / (std / sqrt(T)). */
 int afm_fama_macbeth_f64(afm_ctx* ctx, const double* beta, const int32_t* rank, int64_t nseg,
                          int k, double* mean_out, double* t_out);
+/* Lasso / elastic net by cyclic coordinate descent on centered moments -- replaces
+ * sklearn Lasso(alpha=2e-4, max_iter=10000).fit (KKT:605-607; sklearn's
+ * enet_coordinate_descent_gram, _cd_fast.pyx).  gram: ONE pooled shifted Gram [p+2][p+2] of
+ * [1, x, y] (afm_pool_moments_f64), from which Q = X'X, q = X'y, y'y are centered in-kernel.
+ * Minimises 0.5 ||y - X w||^2 + alpha_n ||w||_1 + 0.5 beta ||w||^2 (alpha_n = sklearn alpha * n)
+ * from w = 0; stops when d_w_max / w_max < tol and the duality gap < tol * y'y, or at max_iter.
+ * w[p] out; info[3] out = {gap, tol * y'y, n_iter}.  p <= 110. */
+int afm_lasso_cd_f64(afm_ctx* ctx, const double* gram, int p, double alpha_n, double beta,
+                     int max_iter, double tol, int positive, double* w, double* info);
 
 /* ---- K1-K3: rebalance, weights, PnL -- replaces PortfolioManager (KKT:795-892) ---------------
  * Book arrays are [nd][2][AFM_MAX_BOOK] (long book, short book). */

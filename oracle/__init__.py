@@ -10,7 +10,7 @@ reference itself (``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``;
 ``tests/test_oracle_golden.py``).  Exceptions, where the reference has no deterministic target,
 are stated per function (the exact box-QP weight solve replaces SLSQP).
 
-Layout: ``factors_oracle.c`` / ``xs_oracle.c`` (plain C, gcc, no FMA contraction) built into
+Layout: ``factors_oracle.c`` / ``xs_oracle.c`` / ``lasso_oracle.c`` (plain C, gcc, no FMA contraction) built into
 ``oracle/build/liboracle.so`` by ``oracle/Makefile``; the pandas-shaped drivers are below and in
 ``oracle/xs.py`` / ``oracle/portfolio.py``.
 """
@@ -69,6 +69,9 @@ def lib():
         L.oracle_nancorr_pair.restype = ctypes.c_double
         L.oracle_group_corr.argtypes = [i64, P, P, P, P]
         L.oracle_group_mean.argtypes = [i64, P, P, i64, P, P, P, P]
+        d = ctypes.c_double
+        L.oracle_lasso_gram.argtypes = [ctypes.c_int, P, P, d, d, d, ctypes.c_int, d,
+                                        ctypes.c_int, P, P, P]
         _lib = L
     return _lib
 
@@ -103,3 +106,29 @@ def compute_factors(data):
     base = data.reset_index(drop=True)
     out = pd.concat([base, pd.DataFrame(fac, columns=FACTOR_NAMES)], axis=1)
     return out.dropna()
+
+
+def lasso_gram(Q, q, ynorm2: float, alpha_n: float, *, max_iter: int = 1000, tol: float = 1e-4,
+               positive: bool = False):
+    """sklearn enet_coordinate_descent_gram restated (oracle/lasso_oracle.c, l2 weight 0):
+    -> (w, gap, tol * y'y, n_iter) on centered moments Q = X'X, q = X'y, ynorm2 = y'y."""
+    Q = np.ascontiguousarray(Q, dtype=np.float64)
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    p = len(q)
+    w = np.zeros(p)
+    H = np.zeros(p)
+    info = np.zeros(3)
+    lib().oracle_lasso_gram(p, _p(Q), _p(q), float(ynorm2), float(alpha_n), 0.0, int(max_iter),
+                            float(tol), int(bool(positive)), _p(w), _p(H), _p(info))
+    return w, float(info[0]), float(info[1]), int(info[2])
+
+
+def centered_moments(G, n_index=True):
+    """Shifted moments G' [p+2][p+2] of [1, x, y] (afm's Gram layout) -> (n, Q, q, y'y): the
+    centered cross-products C = G'[1:,1:] - outer(G'[0,1:], G'[0,1:]) / n."""
+    G = np.asarray(G, dtype=np.float64)
+    n = G[0, 0]
+    g0 = G[0, 1:]
+    C = G[1:, 1:] - np.outer(g0, g0) / n
+    p = G.shape[0] - 2
+    return n, C[:p, :p], C[:p, p], C[p, p]

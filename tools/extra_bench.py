@@ -6,10 +6,12 @@
 * bootstrap -- BASELINE config E: 1,024 bootstrap paths x 5,000 assets: rebalance (books,
                rolling-252 covariance, exact KKT weights) once per date, then every path's
                union alignment, turnover DAGs and value recursion.
+* lasso     -- KKT:605-607 on the config-C pooled train+valid moments (96 factors, ~38 M rows):
+               afm_lasso_cd_f64 with the reference's alpha=2e-4, max_iter=10000, tol=1e-4.
 * intraday  -- BASELINE config D: 3,000 assets x 196,560 one-minute bars (2 years x 252 days x
                390 bars), the 98-column factor build streamed over asset groups sized to HBM
                (afm/intraday.py); algorithmic bytes 816 per present asset-bar.
-Usage: python tools/extra_bench.py [--only zscore|bootstrap|intraday] [--reps N]"""
+Usage: python tools/extra_bench.py [--only zscore|bootstrap|lasso|intraday] [--reps N]"""
 import argparse
 import json
 import os
@@ -82,6 +84,33 @@ def bench_bootstrap(reps, n_paths=1024, A=5000, T=5040):
             "path_steps_per_s": round(n_paths * nd / ((ms_boot) * 1e-3), 1)}
 
 
+def bench_lasso(reps):
+    import torch
+    import afm
+    from afm import _lib
+    from afm.pipeline import Pipeline
+    from afm.synthetic import make_panel
+    A, T = 10000, 5040
+    pipe = Pipeline(afm.PanelGrid.from_panel(make_panel(A, T, seed=2023)))
+    pipe.step()
+    torch.cuda.synchronize()
+    p = pipe.p
+    n = float(pipe.pool_g[0, 0, 0].item())
+    w = torch.empty(p, dtype=torch.float64, device="cuda")
+    info = torch.empty(3, dtype=torch.float64, device="cuda")
+    h = _lib.Context.get(0).bind_stream()
+
+    def run():
+        _lib.check(_lib.lib().afm_lasso_cd_f64(h, _lib.ptr(pipe.pool_g), p, 2e-4 * n, 0.0, 10000,
+                                               1e-4, 0, _lib.ptr(w), _lib.ptr(info)))
+    ms = timed(run, reps)
+    gap, tol_y, it = info.cpu().numpy()
+    return {"stage": "lasso", "workload": f"config C pooled moments: {int(n)} rows x {p} factors, "
+                                          "alpha 2e-4, max_iter 10000, tol 1e-4",
+            "ms": round(ms, 3), "n_iter": int(it), "nonzero": int((w != 0).sum().item()),
+            "us_per_sweep": round(ms * 1e3 / max(it, 1), 2), "converged": bool(gap < tol_y)}
+
+
 def bench_intraday(reps, A=3000, T=2 * 252 * 390):
     import torch
     from afm.intraday import factor_panel_groups, group_blocks, make_panel_device
@@ -105,7 +134,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     for nm, fn in (("zscore", bench_zscore), ("bootstrap", bench_bootstrap),
-                   ("intraday", bench_intraday)):
+                   ("lasso", bench_lasso), ("intraday", bench_intraday)):
         if a.only and a.only != nm:
             continue
         t0 = time.perf_counter()
