@@ -481,6 +481,93 @@ __global__ void xs_series_kernel(int64_t nd, const double* layer_mean, const dou
     }
 }
 
+// ---- §8(f) rank 2: ingest / clean (merge_datasets, KKT:113-166) ---------------------------
+// ffill of each value column per security over the union (date, id) rows in date order
+// (KKT:145): one thread per (column, asset), walking the presence words.
+__global__ __launch_bounds__(256) void ffill_kernel(int64_t K, int64_t T, int64_t lda,
+                                                    double* planes, const uint64_t* bits) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= K * lda) return;
+    const int64_t k = i / lda, a = i - k * lda;
+    double* col = planes + k * T * lda + a;
+    double last = qnan();
+    const int64_t nch = (T + 63) / 64;
+    for (int64_t ch = 0; ch < nch; ++ch) {
+        u64 w = bits[ch * lda + a];
+        while (w) {
+            const int64_t t = ch * 64 + __builtin_ctzll(w);
+            w &= w - 1;
+            double* cell = col + t * lda;
+            const double v = *cell;
+            if (v == v) last = v;
+            else if (last == last) *cell = last;
+        }
+    }
+}
+
+// per-date mean fill (KKT:147): for date t and column k, the NaN cells of the date's rows take
+// the column's mean over those rows -- pandas nanmean: numpy pairwise sum of the rows in
+// security order with NaN -> 0, divided by the non-NaN count (NaN when none).
+__global__ __launch_bounds__(kT) void date_mean_fill_kernel(int64_t K, int64_t T, int64_t A,
+                                                            int64_t lda, double* planes,
+                                                            const uint64_t* bits,
+                                                            double* scratch) {
+    __shared__ PwShared pw;
+    __shared__ int sbuf[kT];
+    __shared__ int cbuf[kT];
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x, k = blockIdx.y;
+    double* row = planes + (k * T + t) * lda;
+    double* scr = scratch + (k * T + t) * lda;
+    int n = 0, cnt = 0;
+    for (int64_t base = 0; base < A; base += kT) {
+        const int64_t a = base + tid;
+        int ok = 0;
+        double v = 0.0;
+        if (a < A && bit_at(bits, lda, t, a)) {
+            ok = 1;
+            v = row[a];
+        }
+        int ex;
+        const int tot = block_scan(ok, sbuf, &ex);
+        if (ok) scr[n + ex] = v == v ? v : 0.0;
+        n += tot;
+        int cex;
+        cnt += block_scan(ok && v == v, cbuf, &cex);
+    }
+    __syncthreads();
+    if (n == 0 || cnt == n) return;                 // no row / nothing to fill (uniform)
+    const double mean = cnt > 0 ? block_np_sum(pw, scr, n) / (double)cnt : qnan();
+    for (int64_t a = tid; a < A; a += kT)
+        if (bit_at(bits, lda, t, a) && !(row[a] == row[a])) row[a] = mean;
+}
+
+// x - mean(x) per group of consecutive rows (Series.mean: numpy pairwise sum / count of the
+// non-NaN values): excess_ret1d per date over the reference rows in file order (KKT:154-161).
+__global__ __launch_bounds__(kT) void group_demean_kernel(const int64_t* offsets, const double* x,
+                                                          double* out, double* scratch) {
+    __shared__ PwShared pw;
+    __shared__ int cbuf[kT];
+    const int tid = threadIdx.x;
+    const int64_t g = blockIdx.x;
+    const int64_t o = offsets[g], n = offsets[g + 1] - o;
+    int cnt = 0;
+    for (int64_t base = 0; base < n; base += kT) {
+        const int64_t i = base + tid;
+        int ok = 0;
+        if (i < n) {
+            const double v = x[o + i];
+            ok = v == v;
+            scratch[o + i] = ok ? v : 0.0;
+        }
+        int ex;
+        cnt += block_scan(ok, cbuf, &ex);
+    }
+    __syncthreads();
+    const double mean = cnt > 0 ? block_np_sum(pw, scratch + o, n) / (double)cnt : qnan();
+    for (int64_t i = tid; i < n; i += kT) out[o + i] = x[o + i] - mean;
+}
+
 }  // namespace
 }  // namespace afm
 
@@ -551,6 +638,45 @@ extern "C" int afm_xs_series_f64(afm_ctx* ctx, int64_t nd, const double* layer_m
     if (nd <= 0) return AFM_OK;
     hipLaunchKernelGGL(xs_series_kernel, dim3(1), dim3(1024), 0, ctx->stream, nd, layer_mean,
                        port, ic, year, nyears, year0, cum_layer, ls, cum_port, ir, scratch);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_ffill_f64(afm_ctx* ctx, int64_t K, int64_t T, int64_t lda, double* planes,
+                             const uint64_t* bits) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(K >= 0 && T >= 0 && lda % 64 == 0, "bad panel shape");
+    AFM_CHECK_ARG(planes && bits, "null buffer");
+    if (K == 0 || T == 0 || lda == 0) return AFM_OK;
+    hipLaunchKernelGGL(ffill_kernel, dim3((unsigned)((K * lda + 255) / 256)), dim3(256), 0,
+                       ctx->stream, K, T, lda, planes, bits);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_date_mean_fill_f64(afm_ctx* ctx, int64_t K, int64_t T, int64_t A, int64_t lda,
+                                      double* planes, const uint64_t* bits, double* scratch) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(K >= 0 && T >= 0 && A >= 0 && A <= lda && lda % 64 == 0, "bad panel shape");
+    AFM_CHECK_ARG(A <= 65536, "at most 65536 securities per date");
+    AFM_CHECK_ARG(K <= 65535, "at most 65535 value columns");
+    AFM_CHECK_ARG(planes && bits && scratch, "null buffer");
+    if (K == 0 || T == 0 || A == 0) return AFM_OK;
+    hipLaunchKernelGGL(date_mean_fill_kernel, dim3((unsigned)T, (unsigned)K), dim3(kT), 0,
+                       ctx->stream, K, T, A, lda, planes, bits, scratch);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_group_demean_f64(afm_ctx* ctx, int64_t ngroups, const int64_t* offsets,
+                                    int64_t max_group, const double* x, double* out,
+                                    double* scratch) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(ngroups >= 0 && max_group <= 65536, "at most 65536 rows per group");
+    AFM_CHECK_ARG(offsets && x && out && scratch, "null buffer");
+    if (ngroups == 0) return AFM_OK;
+    hipLaunchKernelGGL(group_demean_kernel, dim3((unsigned)ngroups), dim3(kT), 0, ctx->stream,
+                       offsets, x, out, scratch);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

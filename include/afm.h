@@ -161,6 +161,22 @@ int afm_bootstrap_pnl_f64(afm_ctx* ctx, int64_t lda, const int32_t* dates, int64
 int afm_min_variance_weights_f64(afm_ctx* ctx, const double* R, int64_t rows, int64_t ld, int k,
                                  double lo, double hi, double* w, double* cov, int32_t* status);
 
+/* ---- §8(f) rank 2: ingest / clean -- replaces merge_datasets' fill steps (KKT:113-166) ------
+ * planes [K][T][lda] value columns on the union (date, id) grid, bits its presence words.
+ * afm_ffill_f64: per security, NaN cells take the last non-NaN value of an earlier present date
+ * (groupby('security_id') ... ffill(), KKT:145).
+ * afm_date_mean_fill_f64: per date and column, NaN cells of present rows take the column mean
+ * over the date's rows (pandas nanmean: numpy pairwise sum in security order with NaN -> 0, over
+ * the non-NaN count; KKT:147).  scratch [K][T][lda].  A <= 65536.
+ * afm_group_demean_f64: out = x - mean(x) per group of consecutive rows [offsets[g], offsets[g+1])
+ * (Series.mean, numpy pairwise; excess_ret1d per date, KKT:154-161).  scratch [n]. */
+int afm_ffill_f64(afm_ctx* ctx, int64_t K, int64_t T, int64_t lda, double* planes,
+                  const uint64_t* bits);
+int afm_date_mean_fill_f64(afm_ctx* ctx, int64_t K, int64_t T, int64_t A, int64_t lda,
+                           double* planes, const uint64_t* bits, double* scratch);
+int afm_group_demean_f64(afm_ctx* ctx, int64_t ngroups, const int64_t* offsets,
+                         int64_t max_group, const double* x, double* out, double* scratch);
+
 /* ---- A1-A4: signal evaluation -- replaces AlphaSignalAnalyzer.run (KKT:298-375) ----------
  * fr [3][T][lda]: k-th next present price row return c'/c - 1 for k = 1, 2, 5, NaN unless <= 1
  * (KKT:311-312); price_bits: presence of price_data rows. */

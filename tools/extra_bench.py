@@ -8,10 +8,13 @@
                union alignment, turnover DAGs and value recursion.
 * lasso     -- KKT:605-607 on the config-C pooled train+valid moments (96 factors, ~38 M rows):
                afm_lasso_cd_f64 with the reference's alpha=2e-4, max_iter=10000, tol=1e-4.
+* ingest    -- merge_datasets' fill steps (KKT:145-161) at config-C scale: 3 value columns on a
+               10,000 x 5,040 union grid (ffill per security + per-date pairwise mean fill) and
+               the per-date excess-return demean over 47.9 M reference rows.
 * intraday  -- BASELINE config D: 3,000 assets x 196,560 one-minute bars (2 years x 252 days x
                390 bars), the 98-column factor build streamed over asset groups sized to HBM
                (afm/intraday.py); algorithmic bytes 816 per present asset-bar.
-Usage: python tools/extra_bench.py [--only zscore|bootstrap|lasso|intraday] [--reps N]"""
+Usage: python tools/extra_bench.py [--only zscore|bootstrap|lasso|ingest|intraday] [--reps N]"""
 import argparse
 import json
 import os
@@ -111,6 +114,44 @@ def bench_lasso(reps):
             "us_per_sweep": round(ms * 1e3 / max(it, 1), 2), "converged": bool(gap < tol_y)}
 
 
+def bench_ingest(reps, A=10000, T=5040, K=3):
+    import torch
+    from afm import _lib
+    from afm.grid import pack_bits
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    lda = (A + 63) // 64 * 64
+    valid = torch.zeros((T, lda), dtype=torch.bool, device="cuda")
+    valid[:, :A] = torch.rand((T, A), generator=g, device="cuda") < 0.95
+    bits = pack_bits(valid)
+    base = torch.randn((K, T, lda), generator=g, dtype=torch.float64, device="cuda")
+    base[torch.rand((K, T, lda), generator=g, device="cuda") < 0.2] = float("nan")
+    planes = base.clone()
+    scratch = torch.empty_like(planes)
+    n = int(valid.sum().item())
+    x = torch.randn(n, generator=g, dtype=torch.float64, device="cuda") * 0.02
+    cnt = valid.sum(dim=1).to(torch.int64)
+    off = torch.zeros(T + 1, dtype=torch.int64, device="cuda")
+    off[1:] = torch.cumsum(cnt, 0)
+    out = torch.empty_like(x)
+    xs = torch.empty_like(x)
+    h = _lib.Context.get(0).bind_stream()
+    L, P = _lib.lib(), _lib.ptr
+
+    def fill():
+        planes.copy_(base)
+        _lib.check(L.afm_ffill_f64(h, K, T, lda, P(planes), P(bits)))
+        _lib.check(L.afm_date_mean_fill_f64(h, K, T, A, lda, P(planes), P(bits), P(scratch)))
+    ms_copy = timed(lambda: planes.copy_(base), reps)
+    ms_fill = timed(fill, reps) - ms_copy
+    ms_dm = timed(lambda: _lib.check(L.afm_group_demean_f64(h, T, P(off), int(cnt.max().item()),
+                                                             P(x), P(out), P(xs))), reps)
+    return {"stage": "ingest", "workload": f"{K} value columns on a {A} x {T} union grid "
+                                           f"({n} rows), excess demean over {n} reference rows",
+            "fill_ms": round(ms_fill, 3), "demean_ms": round(ms_dm, 3),
+            "rows_per_s": round(n / ((ms_fill + ms_dm) * 1e-3), 1)}
+
+
 def bench_intraday(reps, A=3000, T=2 * 252 * 390):
     import torch
     from afm.intraday import factor_panel_groups, group_blocks, make_panel_device
@@ -134,7 +175,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     for nm, fn in (("zscore", bench_zscore), ("bootstrap", bench_bootstrap),
-                   ("lasso", bench_lasso), ("intraday", bench_intraday)):
+                   ("lasso", bench_lasso), ("ingest", bench_ingest),
+                   ("intraday", bench_intraday)):
         if a.only and a.only != nm:
             continue
         t0 = time.perf_counter()
