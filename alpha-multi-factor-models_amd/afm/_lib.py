@@ -39,6 +39,7 @@ SIGNATURES = {
     "afm_vec_add_f64": (I32, [P, I64, P, P]),
     "afm_ols_intercept_f64": (I32, [P, I32, P, P]),
     "afm_lasso_cd_f64": (I32, [P, P, I32, DBL, DBL, I32, DBL, I32, P, P]),
+    "afm_talib_factors_f64": (I32, [P, I64, I64, I64, P, P, P, P]),
     "afm_ffill_f64": (I32, [P, I64, I64, I64, P, P]),
     "afm_date_mean_fill_f64": (I32, [P, I64, I64, I64, I64, P, P, P]),
     "afm_group_demean_f64": (I32, [P, I64, P, I64, P, P, P]),

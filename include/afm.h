@@ -161,6 +161,15 @@ int afm_bootstrap_pnl_f64(afm_ctx* ctx, int64_t lda, const int32_t* dates, int64
 int afm_min_variance_weights_f64(afm_ctx* ctx, const double* R, int64_t rows, int64_t ld, int k,
                                  double lo, double hi, double* w, double* cov, int32_t* status);
 
+/* ---- §8(f) rank 3: the talib factor variant (KKT:176-270) ------------------------------------
+ * The 68 TA-Lib-defined columns for a calendar-grid panel (inputs as afm_factors_f64), out
+ * [68][T][lda]: SMA_i 0-11, EMA_i 12-23, VSMA_i 24-35 (i = 6..50 step 4), BBANDS upper / middle /
+ * lower 36-59 (i = 14..56 step 6), MACD_12_{18,24,30} 60-62, RSI_{8,14,20} 63-65, PVT 66, OBV 67
+ * (TA-Lib 0.4 C-core semantics restated -- see csrc/talib.hip; the shared pandas columns come from
+ * afm_factors_f64).  Absent cells are not written. */
+int afm_talib_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, const double* close,
+                          const double* volume, const uint64_t* valid_bits, double* out);
+
 /* ---- §8(f) rank 2: ingest / clean -- replaces merge_datasets' fill steps (KKT:113-166) ------
  * planes [K][T][lda] value columns on the union (date, id) grid, bits its presence words.
  * afm_ffill_f64: per security, NaN cells take the last non-NaN value of an earlier present date

@@ -10,7 +10,7 @@ reference itself (``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``;
 ``tests/test_oracle_golden.py``).  Exceptions, where the reference has no deterministic target,
 are stated per function (the exact box-QP weight solve replaces SLSQP).
 
-Layout: ``factors_oracle.c`` / ``xs_oracle.c`` / ``lasso_oracle.c`` (plain C, gcc, no FMA contraction) built into
+Layout: ``factors_oracle.c`` / ``xs_oracle.c`` / ``lasso_oracle.c`` / ``talib_oracle.c`` (plain C, gcc, no FMA contraction) built into
 ``oracle/build/liboracle.so`` by ``oracle/Makefile``; the pandas-shaped drivers are below and in
 ``oracle/xs.py`` / ``oracle/portfolio.py``.
 """
@@ -72,6 +72,7 @@ def lib():
         d = ctypes.c_double
         L.oracle_lasso_gram.argtypes = [ctypes.c_int, P, P, d, d, d, ctypes.c_int, d,
                                         ctypes.c_int, P, P, P]
+        L.oracle_talib_panel.argtypes = [i64, P, P, P, P, P]
         _lib = L
     return _lib
 
@@ -132,3 +133,20 @@ def centered_moments(G, n_index=True):
     C = G[1:, 1:] - np.outer(g0, g0) / n
     p = G.shape[0] - 2
     return n, C[:p, :p], C[:p, p], C[p, p]
+
+
+TALIB_COLS = 68
+
+
+def talib_factors_long(offsets: np.ndarray, close, volume) -> np.ndarray:
+    """TA-Lib columns of the talib variant (oracle/talib_oracle.c; parity with TA-Lib itself is
+    unpinned): rows sorted by (security, date), CSR ``offsets`` -> ``[n_rows][68]``."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    c = np.ascontiguousarray(close, dtype=np.float64)
+    v = np.ascontiguousarray(volume, dtype=np.float64)
+    n = int(offsets[-1])
+    out = np.empty((n, TALIB_COLS), dtype=np.float64)
+    longest = int(np.diff(offsets).max()) if len(offsets) > 1 else 0
+    work = np.empty(4 * max(longest, 1), dtype=np.float64)
+    lib().oracle_talib_panel(len(offsets) - 1, _p(offsets), _p(c), _p(v), _p(out), _p(work))
+    return out

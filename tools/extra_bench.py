@@ -11,10 +11,12 @@
 * ingest    -- merge_datasets' fill steps (KKT:145-161) at config-C scale: 3 value columns on a
                10,000 x 5,040 union grid (ffill per security + per-date pairwise mean fill) and
                the per-date excess-return demean over 47.9 M reference rows.
+* talib     -- the 68 TA-Lib columns of the talib variant (KKT:176-270) on the config-C panel;
+               algorithmic bytes 16 read + 68 x 8 written per present asset-day.
 * intraday  -- BASELINE config D: 3,000 assets x 196,560 one-minute bars (2 years x 252 days x
                390 bars), the 98-column factor build streamed over asset groups sized to HBM
                (afm/intraday.py); algorithmic bytes 816 per present asset-bar.
-Usage: python tools/extra_bench.py [--only zscore|bootstrap|lasso|ingest|intraday] [--reps N]"""
+Usage: python tools/extra_bench.py [--only zscore|bootstrap|lasso|ingest|talib|intraday] [--reps N]"""
 import argparse
 import json
 import os
@@ -152,6 +154,21 @@ def bench_ingest(reps, A=10000, T=5040, K=3):
             "rows_per_s": round(n / ((ms_fill + ms_dm) * 1e-3), 1)}
 
 
+def bench_talib(reps, A=10000, T=5040):
+    import torch
+    import afm
+    from afm.synthetic import make_panel
+    from afm.talib_factors import TALIB_COLS, talib_panel
+    g = afm.PanelGrid.from_panel(make_panel(A, T, seed=2023))
+    out = torch.empty((TALIB_COLS, T, g.lda), dtype=torch.float64, device="cuda")
+    ms = timed(lambda: talib_panel(g, out), reps)
+    n = g.n_asset_days()
+    byts = (16 + 8 * TALIB_COLS) * n
+    return {"stage": "talib", "workload": f"{A} assets x {T} days, {TALIB_COLS} TA-Lib columns",
+            "ms": round(ms, 3), "asset_days_per_s": round(n / (ms * 1e-3), 1),
+            "GBps": round(byts / (ms * 1e-3) / 1e9, 1)}
+
+
 def bench_intraday(reps, A=3000, T=2 * 252 * 390):
     import torch
     from afm.intraday import factor_panel_groups, group_blocks, make_panel_device
@@ -175,7 +192,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     for nm, fn in (("zscore", bench_zscore), ("bootstrap", bench_bootstrap),
-                   ("lasso", bench_lasso), ("ingest", bench_ingest),
+                   ("lasso", bench_lasso), ("ingest", bench_ingest), ("talib", bench_talib),
                    ("intraday", bench_intraday)):
         if a.only and a.only != nm:
             continue
