@@ -13,8 +13,10 @@ One ``step()`` over a device-resident calendar-grid panel:
                  pairwise covariance, exact box-QP weights (KKT:842-892)
 7. pnl           afm_pnl_scan_f64: value / turnover recursion
 
-All buffers are allocated once; every stage runs on torch's current stream, so a step is a
-straight sequence of kernel launches (no host synchronisation inside).
+All buffers are allocated once and there is no host synchronisation inside a step.  Every
+stage runs on torch's current stream except stage 3: no later stage reads its results, so it
+runs on a side stream (forked after stage 2, joined at the end of the step) and overlaps
+stages 4-7, whose last one, the PnL scan, occupies a single CU.
 """
 from __future__ import annotations
 
@@ -62,6 +64,7 @@ class Pipeline:
         self.out = torch.empty((N_FACTORS, T, lda), **f64)
         self.nanfree = torch.zeros((nch, lda), **i64)
         self.finite = torch.zeros((nch, lda), **i64)
+        self.rows = torch.zeros((nch, lda), **i64)     # finite rows with a label (Gram rows)
         self.cols = torch.as_tensor(np.asarray(self.cfg.cols, dtype=np.int32), device=dev)
         self.gram = torch.empty((T, p2, p2), **f64)
         self.shift = torch.empty((T, p2), **f64)
@@ -93,6 +96,9 @@ class Pipeline:
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         self.ctx = _lib.Context.get(dev.index)
+        # the per-date solve + Fama-MacBeth (results nobody downstream reads) run on a side
+        # stream, overlapping pooled OLS -> predict -> rebalance -> the one-CU PnL scan
+        self.side = torch.cuda.Stream(device=dev)
 
     def step(self, events: dict | None = None, only=None):
         """One pass of the hot path.  ``events``: optional {stage: (start, end)} CUDA events.
@@ -116,19 +122,29 @@ class Pipeline:
             mark("factors", 0)
             chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), P(g.ret1d), P(g.excess),
                                   P(g.vbits), P(self.out), P(self.nanfree), P(self.finite)), "factors")
+            chk(L.afm_drop_last_obs_bits(h, T, lda, P(g.vbits), P(self.finite), P(self.rows)),
+                "label rows")
             mark("factors", 1)
         if on("xs_gram"):
             mark("xs_gram", 0)
             chk(L.afm_xs_gram_f64(h, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p, c.ycol,
-                                  P(self.finite), 0, T, P(self.gram), P(self.shift)), "xs_gram")
+                                  P(self.rows), 0, T, P(self.gram), P(self.shift)), "xs_gram")
             mark("xs_gram", 1)
+        joined = None
         if on("xs_solve"):
-            mark("xs_solve", 0)
-            chk(L.afm_ols_solve_f64(h, P(self.gram), P(self.shift), p, T, c.tol, P(self.beta),
-                                    P(self.nobs), P(self.rank)), "ols_solve")
-            chk(L.afm_fama_macbeth_f64(h, P(self.beta), P(self.rank), T, p + 1, P(self.fm_mean),
-                                       P(self.fm_t)), "fama_macbeth")
-            mark("xs_solve", 1)
+            import torch
+            main = torch.cuda.current_stream(self.g.device)
+            self.side.wait_stream(main)                    # after the Grams
+            with torch.cuda.stream(self.side):
+                hs = self.ctx.bind_stream()
+                mark("xs_solve", 0)
+                chk(L.afm_ols_solve_f64(hs, P(self.gram), P(self.shift), p, T, c.tol,
+                                        P(self.beta), P(self.nobs), P(self.rank)), "ols_solve")
+                chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1,
+                                           P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
+                mark("xs_solve", 1)
+            joined = main
+            h = self.ctx.bind_stream()
         if on("pooled_ols"):
             mark("pooled_ols", 0)
             chk(L.afm_pool_moments_f64(h, P(self.gram), P(self.shift), p, self.t_test,
@@ -160,6 +176,8 @@ class Pipeline:
                                    P(r["usize"]), 100000000.0, c.rate, P(q["value"]),
                                    P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])), "pnl")
             mark("pnl", 1)
+        if joined is not None:
+            joined.wait_stream(self.side)                 # the step ends when both are done
 
     def summary(self) -> dict:
         """Host copies of the headline results (after a synchronize)."""

@@ -125,6 +125,7 @@ class ShardedPipeline:
         self.out = torch.empty((N_FACTORS, T, self.lda_r), **f64)
         self.nanfree = torch.zeros((nch, self.lda_r), **i64)
         self.finite = torch.zeros((nch, self.lda_r), **i64)
+        self.rows = torch.zeros((nch, self.lda_r), **i64)
         self.cols = torch.as_tensor(np.asarray(c.cols, dtype=np.int32), device=dev)
         p2 = self.p2
         self.gram_r = torch.empty((T, p2, p2), **f64)           # partial moments, all dates
@@ -214,13 +215,15 @@ class ShardedPipeline:
         chk(L.afm_factors_f64(h, T, self.A_r, lr, P(g.close), P(g.volume), P(g.ret1d),
                               P(g.excess), P(g.vbits), P(self.out), P(self.nanfree),
                               P(self.finite)), "factors")
+        chk(L.afm_drop_last_obs_bits(h, T, lr, P(g.vbits), P(self.finite), P(self.rows)),
+            "label rows")
         f = self.full
         chk(L.afm_labels_f64(h, T, lda, self.lab0, T, P(f.excess), P(f.ret1d), P(f.vbits),
                              P(self.target), P(self.tmr)), "labels")
         mark("factors", 1)
         mark("xs_gram", 0)
         chk(L.afm_xs_gram_f64(h, P(self.out), T * lr, lr, self.A_r, -1, P(self.cols), p, c.ycol,
-                              P(self.finite), 0, T, P(self.gram_r), P(self.shift_r)), "xs_gram")
+                              P(self.rows), 0, T, P(self.gram_r), P(self.shift_r)), "xs_gram")
         mark("xs_gram", 1)
         # ---- exchange: each date's per-rank partial moments -> the date's owner ----
         mark("exchange", 0)

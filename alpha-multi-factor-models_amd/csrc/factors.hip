@@ -1114,6 +1114,25 @@ __global__ __launch_bounds__(256) void labels_kernel(int64_t T, int64_t t_begin,
     }
 }
 
+// out = in without each asset's last present day: the rows whose shift(-1) labels (target,
+// tmr_ret1d, No-talib.py:90-91) are NaN.  One thread per asset; words copied coalesced.
+__global__ __launch_bounds__(256) void drop_last_obs_kernel(int64_t nwords, int64_t lda,
+                                                            const uint64_t* vbits,
+                                                            const uint64_t* in, uint64_t* out) {
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a >= lda) return;
+    int64_t last = -1;
+    for (int64_t c = nwords - 1; c >= 0 && last < 0; --c) {
+        const u64 w = vbits[c * lda + a];
+        if (w) last = c * 64 + 63 - __builtin_clzll(w);
+    }
+    for (int64_t c = 0; c < nwords; ++c) {
+        u64 w = in[c * lda + a];
+        if (last >= 0 && (last >> 6) == c) w &= ~(1ull << (last & 63));
+        out[c * lda + a] = w;
+    }
+}
+
 }  // namespace
 }  // namespace afm
 
@@ -1233,6 +1252,18 @@ extern "C" int afm_labels_f64(afm_ctx* ctx, int64_t T, int64_t lda, int64_t t0, 
     dim3 g2((unsigned)(lda / 64), (unsigned)((t1 - t0 + 3) / 4));
     hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, t0, t1, lda, excess,
                        ret1d, valid_bits, target, tmr);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_drop_last_obs_bits(afm_ctx* ctx, int64_t T, int64_t lda,
+                                      const uint64_t* valid_bits, const uint64_t* in_bits,
+                                      uint64_t* out_bits) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && lda > 0 && lda % 64 == 0, "bad panel shape");
+    AFM_CHECK_ARG(valid_bits && in_bits && out_bits, "null buffer");
+    hipLaunchKernelGGL(afm::drop_last_obs_kernel, dim3((unsigned)((lda + 255) / 256)), dim3(256),
+                       0, ctx->stream, (T + 63) / 64, lda, valid_bits, in_bits, out_bits);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

@@ -59,6 +59,11 @@ int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                     const double* excess, const uint64_t* valid_bits,
                     double* out, uint64_t* nanfree_bits, uint64_t* finite_bits);
 
+/* out_bits = in_bits without each asset's last present day (valid_bits): the rows whose
+ * shift(-1) labels are NaN.  Used to mask the regression rows up front (the Gram's REDO pass
+ * would otherwise re-run those dates). */
+int afm_drop_last_obs_bits(afm_ctx* ctx, int64_t T, int64_t lda, const uint64_t* valid_bits,
+                           const uint64_t* in_bits, uint64_t* out_bits);
 /* target = excess_ret1d.shift(-1), tmr_ret1d = ret1d.shift(-1) per asset (No-talib.py:90-91) for
  * the grid dates [t0, t1) only (the label planes of afm_factors_f64 for a sub-range; used where
  * the factor panel itself is sharded by asset but the history/PnL planes are needed for every
