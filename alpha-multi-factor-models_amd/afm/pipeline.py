@@ -13,10 +13,11 @@ One ``step()`` over a device-resident calendar-grid panel:
                  pairwise covariance, exact box-QP weights (KKT:842-892)
 7. pnl           afm_pnl_scan_f64: value / turnover recursion
 
-All buffers are allocated once and there is no host synchronisation inside a step.  Every
-stage runs on torch's current stream except stage 3: no later stage reads its results, so it
-runs on a side stream (forked after stage 2, joined at the end of the step) and overlaps
-stages 4-7, whose last one, the PnL scan, occupies a single CU.
+All buffers are allocated once and there is no host synchronisation inside a step.  Stages
+4-7 need only the Grams of the train+valid dates, and nothing downstream reads stage 3.  So the
+main stream runs 1 -> 2 (train+valid dates) -> 4 -> 7 while a side stream, forked after that
+Gram and joined at the end of the step, runs the test dates' Grams and stage 3.  The side work
+fills the GPU while the main chain runs its latency-bound tail (the PnL scan uses one CU).
 """
 from __future__ import annotations
 
@@ -30,6 +31,9 @@ from .grid import PanelGrid
 from .portfolio import MAX_BOOK
 
 STAGES = ("factors", "xs_gram", "xs_solve", "pooled_ols", "predict", "rebalance", "pnl")
+# single-device step: xs_gram covers the train+valid dates (what the pooled OLS needs), the test
+# dates' Grams (xs_gram_test) run on the side stream ahead of the per-date solve
+PIPELINE_STAGES = STAGES + ("xs_gram_test",)
 
 
 @dataclass
@@ -125,24 +129,32 @@ class Pipeline:
             chk(L.afm_drop_last_obs_bits(h, T, lda, P(g.vbits), P(self.finite), P(self.rows)),
                 "label rows")
             mark("factors", 1)
-        if on("xs_gram"):
+        tt = self.t_test
+        if on("xs_gram"):                                  # train + valid dates
             mark("xs_gram", 0)
             chk(L.afm_xs_gram_f64(h, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p, c.ycol,
-                                  P(self.rows), 0, T, P(self.gram), P(self.shift)), "xs_gram")
+                                  P(self.rows), 0, tt, P(self.gram), P(self.shift)), "xs_gram")
             mark("xs_gram", 1)
         joined = None
-        if on("xs_solve"):
+        if on("xs_solve") or on("xs_gram_test"):
             import torch
             main = torch.cuda.current_stream(self.g.device)
-            self.side.wait_stream(main)                    # after the Grams
+            self.side.wait_stream(main)                    # after the train+valid Grams
             with torch.cuda.stream(self.side):
                 hs = self.ctx.bind_stream()
-                mark("xs_solve", 0)
-                chk(L.afm_ols_solve_f64(hs, P(self.gram), P(self.shift), p, T, c.tol,
-                                        P(self.beta), P(self.nobs), P(self.rank)), "ols_solve")
-                chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1,
-                                           P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
-                mark("xs_solve", 1)
+                mark("xs_gram_test", 0)                    # test dates
+                chk(L.afm_xs_gram_f64(hs, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p,
+                                      c.ycol, P(self.rows), tt, T - tt, P(self.gram[tt:]),
+                                      P(self.shift[tt:])), "xs_gram_test")
+                mark("xs_gram_test", 1)
+                if on("xs_solve"):
+                    mark("xs_solve", 0)
+                    chk(L.afm_ols_solve_f64(hs, P(self.gram), P(self.shift), p, T, c.tol,
+                                            P(self.beta), P(self.nobs), P(self.rank)),
+                        "ols_solve")
+                    chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1,
+                                               P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
+                    mark("xs_solve", 1)
             joined = main
             h = self.ctx.bind_stream()
         if on("pooled_ols"):

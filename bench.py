@@ -118,7 +118,7 @@ def main():
     import torch.distributed as dist
 
     import afm
-    from afm.pipeline import STAGES, Pipeline
+    from afm.pipeline import PIPELINE_STAGES, Pipeline
     from afm.synthetic import make_panel
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,7 +141,7 @@ def main():
         n_ad_local = pipe.n_asset_days_local()
     else:
         pipe = Pipeline(grid)
-        stages = STAGES
+        stages = PIPELINE_STAGES
         n_ad_local = n_ad
     torch.cuda.synchronize()
     log(f"[rank {rank}] panel {grid.A}x{grid.T} ({n_ad} asset-days, {n_ad_local} in this rank's "
@@ -181,7 +181,10 @@ def main():
         # roofline of the dominant kernel: factor panel (HBM) or the per-date Gram (fp64 MFMA)
         p = pipe.p
         fac_gbs = FACTOR_BYTES_PER_AD * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
-        gram_rows = float(pipe.nobs.sum().item()) / world      # this rank's share of the rows
+        if world == 1:      # stage xs_gram = the train+valid dates (the test dates: side stream)
+            gram_rows = float(pipe.nobs[:pipe.t_test].sum().item())
+        else:
+            gram_rows = float(pipe.nobs.sum().item()) / world  # this rank's share of the rows
         gram_tfs = gram_rows * (p + 2) * (p + 3) / (stage_ms["xs_gram"] * 1e-3) / 1e12
         single = world == 1
         if stage_ms["factors"] >= stage_ms["xs_gram"]:

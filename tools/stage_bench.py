@@ -19,7 +19,7 @@ def main():
     args = ap.parse_args()
     import torch
     import afm
-    from afm.pipeline import STAGES, Pipeline
+    from afm.pipeline import PIPELINE_STAGES as STAGES, Pipeline
     from afm.synthetic import make_panel
     torch.cuda.set_device(0)
     grid = afm.PanelGrid.from_panel(make_panel(args.assets, args.days, seed=2023))
