@@ -914,14 +914,21 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                     lds_sync();
                     const int* adds = R + 4 + m;
                     const int* lend = adds + nint;
+                    // one DAG level per step; the next level's first add descriptor is fetched
+                    // while this level's node reads are in flight (descriptors are value-free)
                     int st = 0;
-                    for (int l = 0; l < L; ++l) {                     // one DAG level per step
-                        const int en = lend[l];
+                    int en = L > 0 ? lend[0] : 0;
+                    int wcur = lane < en ? adds[lane] : 0;
+                    for (int l = 0; l < L; ++l) {
+                        const int en2 = l + 1 < L ? lend[l + 1] : en;
+                        const int wnext = en + lane < en2 ? adds[en + lane] : 0;
                         for (int e = st + lane; e < en; e += 64) {
-                            const int w = adds[e];
+                            const int w = e == st + lane ? wcur : adds[e];
                             node[m + e] = node[w & 0xffff] + node[w >> 16];
                         }
                         st = en;
+                        en = en2;
+                        wcur = wnext;
                         lds_sync();
                     }
                     to = node[nint > 0 ? m + nint - 1 : 0] / 2;
