@@ -73,6 +73,20 @@ class Comm:
             self.dist.all_gather_into_tensor(out, src, group=self.group)
         return out.to(t.device)
 
+    def all_gather_packed(self, tensors):
+        """Several equal-shape-per-rank tensors of any dtypes in ONE all-gather (their bytes
+        concatenated) -> list of [world, *t.shape] tensors."""
+        import torch
+        flat = [t.contiguous().view(-1).view(torch.uint8) for t in tensors]
+        sizes = [f.numel() for f in flat]
+        g = self.all_gather(torch.cat(flat))                     # [world, total bytes]
+        out, off = [], 0
+        for t, n in zip(tensors, sizes):
+            part = g[:, off:off + n].contiguous().view(t.dtype)
+            out.append(part.view((self.world,) + tuple(t.shape)))
+            off += n
+        return out
+
     def all_to_all(self, inp, in_splits, out_splits):
         """all_to_all_single along dim 0 with explicit split sizes (rows)."""
         import torch
@@ -241,9 +255,7 @@ class ShardedPipeline:
             chk(L.afm_ols_solve_f64(h, P(self.gram), P(self.shift), p, self.nd_own, c.tol,
                                     P(self.beta_own), P(self.nobs_own), P(self.rank_own)),
                 "ols_solve")
-        bg = cm.all_gather(self.beta_own)
-        ng = cm.all_gather(self.nobs_own)
-        kg = cm.all_gather(self.rank_own)
+        bg, ng, kg = cm.all_gather_packed([self.beta_own, self.nobs_own, self.rank_own])
         for q, (lo, hi) in enumerate(self.drange):
             self.beta[lo:hi] = bg[q, :hi - lo]
             self.nobs[lo:hi] = ng[q, :hi - lo]
@@ -260,8 +272,9 @@ class ShardedPipeline:
         if ntr > 0:
             chk(L.afm_pool_segments_f64(h, P(self.gram), P(self.shift), p, ntr, 64,
                                         P(self.blk_g), P(self.blk_s)), "pool blocks")
-        ag = cm.all_gather(self.blk_g).reshape(W * self.nb_max, p2, p2).contiguous()
-        as_ = cm.all_gather(self.blk_s).reshape(W * self.nb_max, p2).contiguous()
+        ag, as_ = cm.all_gather_packed([self.blk_g, self.blk_s])
+        ag = ag.reshape(W * self.nb_max, p2, p2).contiguous()
+        as_ = as_.reshape(W * self.nb_max, p2).contiguous()
         h = self.ctx.bind_stream()
         chk(L.afm_pool_segments_f64(h, P(ag), P(as_), p, W * self.nb_max, W * self.nb_max,
                                     P(self.pool_g), P(self.pool_s)), "pool")
@@ -296,13 +309,15 @@ class ShardedPipeline:
                                     P(x["status"])), "rebalance")
         lo = self.i0 - self.e0
         n_own = self.i1 - self.i0
+        owns = []
         for k, v in x.items():
             own = v[lo:lo + n_own]
             if n_own < self.nr_max:
                 pad = torch.zeros((self.nr_max - n_own,) + tuple(v.shape[1:]), dtype=v.dtype,
                                   device=v.device)
                 own = torch.cat([own, pad])
-            gath = cm.all_gather(own)
+            owns.append(own)
+        for k, gath in zip(x.keys(), cm.all_gather_packed(owns)):    # one collective
             for q, (qlo, qhi) in enumerate(self.rrange):
                 self.reb[k][qlo:qhi] = gath[q, :qhi - qlo]
         mark("rebalance", 1)

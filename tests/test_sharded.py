@@ -65,6 +65,15 @@ def _comm_worker(rank, world, port, outdir):
     for s, n in enumerate(outs):
         assert (y[off:off + n] == 100.0 * s + rank).all()
         off += n
+    # several dtypes in one packed all-gather
+    a = torch.arange(6, dtype=torch.int32).view(2, 3) + 10 * rank
+    b = torch.full((5,), 0.5 + rank, dtype=torch.float64)
+    c = torch.tensor([rank], dtype=torch.int64)
+    ga, gb, gc = cm.all_gather_packed([a, b, c])
+    for q in range(world):
+        assert torch.equal(ga[q], torch.arange(6, dtype=torch.int32).view(2, 3) + 10 * q)
+        assert torch.equal(gb[q], torch.full((5,), 0.5 + q, dtype=torch.float64))
+        assert int(gc[q, 0]) == q
     cm.barrier()
     open(os.path.join(outdir, f"ok{rank}"), "w").write("ok")
 
