@@ -144,6 +144,12 @@ class ShardedPipeline:
         p2 = self.p2
         self.gram_r = torch.empty((T, p2, p2), **f64)           # partial moments, all dates
         self.shift_r = torch.empty((T, p2), **f64)
+        # the Grams are exactly symmetric (gram_kernel writes both halves from one value): only
+        # the upper triangle + the shift travel in the exchange (half the bytes)
+        iu = torch.triu_indices(p2, p2)
+        self.tri = (iu[0] * p2 + iu[1]).to(dev)
+        self.tri_t = (iu[1] * p2 + iu[0]).to(dev)
+        self.ntri = int(self.tri.numel())
         # ---- date shards (64-date blocks) ----
         self.drange = [block_range(T, W, q) for q in range(W)]
         d0, d1 = self.drange[r]
@@ -242,8 +248,13 @@ class ShardedPipeline:
         # ---- exchange: each date's per-rank partial moments -> the date's owner ----
         mark("exchange", 0)
         W = cm.world
-        rg = cm.all_to_all(self.gram_r.view(T, p2 * p2), self.nd_q, [self.nd_own] * W)
-        rs = cm.all_to_all(self.shift_r, self.nd_q, [self.nd_own] * W)
+        send = torch.cat([self.gram_r.view(T, p2 * p2).index_select(1, self.tri), self.shift_r],
+                         dim=1)
+        recv = cm.all_to_all(send, self.nd_q, [self.nd_own] * W)  # [W * nd_own][ntri + p2]
+        rs = recv[:, self.ntri:]
+        rg = torch.empty((recv.shape[0], p2 * p2), dtype=recv.dtype, device=recv.device)
+        rg[:, self.tri] = recv[:, :self.ntri]
+        rg[:, self.tri_t] = recv[:, :self.ntri]
         mark("exchange", 1)
         h = self.ctx.bind_stream()
         mark("xs_solve", 0)
