@@ -870,23 +870,40 @@ __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, cons
 }
 
 // ---- predictions: pred[t][a] = beta0 + sum_j beta_j x_j (grid rows with a set mask bit) ------
+// HBM-bound: 8 B per regressor per test cell.  The column offsets are staged once per workgroup
+// in LDS and each lane issues kPredBatch independent plane loads before folding them into the
+// sum in order (s = s + b_j x_j, j ascending: the same operations as a plain loop), so a wave keeps
+// a batch of loads in flight instead of one dependent load per regressor.
+constexpr int kPredBatch = 16;
 __global__ __launch_bounds__(256) void predict_kernel(const double* base, int64_t col_stride,
                                                       int64_t lda, int64_t t0, int64_t nt,
                                                       const int32_t* cols, int p,
                                                       const double* beta, int64_t beta_stride,
                                                       const uint64_t* bits, int ycheck,
                                                       double* pred) {
+    __shared__ int64_t coff[kMaxF];
+    for (int j = threadIdx.x; j < p; j += 256) coff[j] = (int64_t)cols[j] * col_stride;
+    __syncthreads();
     const int64_t a = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
     const int64_t t = t0 + (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
     if (t >= t0 + nt) return;
     const double* b = beta + (t - t0) * beta_stride;
+    const double* cell = base + t * lda + a;
     u64 w = bits[(t >> 6) * lda + a];
     double v = __builtin_nan("");
     bool use = (w >> (t & 63)) & 1ull;
-    if (use && ycheck >= 0) use = __builtin_isfinite(base[(int64_t)ycheck * col_stride + t * lda + a]);
+    if (use && ycheck >= 0) use = __builtin_isfinite(cell[(int64_t)ycheck * col_stride]);
     if (use) {
         double s = b[0];
-        for (int j = 0; j < p; ++j) s = s + b[1 + j] * base[(int64_t)cols[j] * col_stride + t * lda + a];
+        int j = 0;
+        for (; j + kPredBatch <= p; j += kPredBatch) {
+            double x[kPredBatch];
+#pragma unroll
+            for (int k = 0; k < kPredBatch; ++k) x[k] = cell[coff[j + k]];
+#pragma unroll
+            for (int k = 0; k < kPredBatch; ++k) s = s + b[1 + j + k] * x[k];
+        }
+        for (; j < p; ++j) s = s + b[1 + j] * cell[coff[j]];
         v = s;
     }
     pred[t * lda + a] = v;
@@ -1083,6 +1100,7 @@ extern "C" int afm_predict_f64(afm_ctx* ctx, const double* base, int64_t col_str
     AFM_CTX(ctx);
     AFM_CHECK_ARG(base && cols && beta && bits && pred, "null buffer");
     AFM_CHECK_ARG(lda % 64 == 0 && nt >= 0 && t0 >= 0, "bad shape");
+    AFM_CHECK_ARG(p >= 0 && p <= kMaxF, "need 0 <= p <= 112");
     if (nt == 0) return AFM_OK;
     dim3 grid((unsigned)(lda / 64), (unsigned)((nt + 3) / 4));
     hipLaunchKernelGGL(predict_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride, lda, t0,
