@@ -26,7 +26,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from .factors import N_FACTORS, TARGET
+from .factors import N_FACTORS, TARGET, TMR
 from .grid import PanelGrid
 from .portfolio import MAX_BOOK
 
@@ -100,9 +100,14 @@ class Pipeline:
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         self.ctx = _lib.Context.get(dev.index)
-        # the per-date solve + Fama-MacBeth (results nobody downstream reads) run on a side
-        # stream, overlapping pooled OLS -> predict -> rebalance -> the one-CU PnL scan
-        self.side = torch.cuda.Stream(device=dev)
+        # the step's latency-critical chain runs on a high-priority stream; the label planes
+        # (next to the factor kernel) and the test dates' Grams + per-date solve + Fama-MacBeth
+        # (results nobody downstream reads) run on a low-priority side stream, so the queue
+        # arbiter hands freed CU slots to the main chain first (AFM_PIPE_PRIO=0: equal priority)
+        import os
+        prio = os.environ.get("AFM_PIPE_PRIO", "1") != "0"
+        self.main = torch.cuda.Stream(device=dev, priority=-8 if prio else 0)
+        self.side = torch.cuda.Stream(device=dev, priority=0)
 
     def step(self, events: dict | None = None, only=None):
         """One pass of the hot path.  ``events``: optional {stage: (start, end)} CUDA events.
@@ -113,7 +118,10 @@ class Pipeline:
         chk = _lib.check
         g, c = self.g, self.cfg
         T, lda, p = self.T, self.lda, self.p
-        h = self.ctx.bind_stream()
+        import torch
+        caller = torch.cuda.current_stream(g.device)
+        self.main.wait_stream(caller)
+        self.side.wait_stream(caller)
 
         def mark(stage, which):
             if events is not None:
@@ -122,74 +130,85 @@ class Pipeline:
         def on(stage):
             return only is None or stage in only
 
-        if on("factors"):
-            mark("factors", 0)
-            chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), P(g.ret1d), P(g.excess),
-                                  P(g.vbits), P(self.out), P(self.nanfree), P(self.finite)), "factors")
-            chk(L.afm_drop_last_obs_bits(h, T, lda, P(g.vbits), P(self.finite), P(self.rows)),
-                "label rows")
-            mark("factors", 1)
-        tt = self.t_test
-        if on("xs_gram"):                                  # train + valid dates
-            mark("xs_gram", 0)
-            chk(L.afm_xs_gram_f64(h, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p, c.ycol,
-                                  P(self.rows), 0, tt, P(self.gram), P(self.shift)), "xs_gram")
-            mark("xs_gram", 1)
-        joined = None
-        if on("xs_solve") or on("xs_gram_test"):
-            import torch
-            main = torch.cuda.current_stream(self.g.device)
-            self.side.wait_stream(main)                    # after the train+valid Grams
-            with torch.cuda.stream(self.side):
-                hs = self.ctx.bind_stream()
-                mark("xs_gram_test", 0)                    # test dates
-                chk(L.afm_xs_gram_f64(hs, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p,
-                                      c.ycol, P(self.rows), tt, T - tt, P(self.gram[tt:]),
-                                      P(self.shift[tt:])), "xs_gram_test")
-                mark("xs_gram_test", 1)
-                if on("xs_solve"):
-                    mark("xs_solve", 0)
-                    chk(L.afm_ols_solve_f64(hs, P(self.gram), P(self.shift), p, T, c.tol,
-                                            P(self.beta), P(self.nobs), P(self.rank)),
-                        "ols_solve")
-                    chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1,
-                                               P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
-                    mark("xs_solve", 1)
-            joined = main
+        with torch.cuda.stream(self.main):
             h = self.ctx.bind_stream()
-        if on("pooled_ols"):
-            mark("pooled_ols", 0)
-            chk(L.afm_pool_moments_f64(h, P(self.gram), P(self.shift), p, self.t_test,
-                                       P(self.pool_g), P(self.pool_s)), "pool")
-            chk(L.afm_ols_solve_f64(h, P(self.pool_g), P(self.pool_s), p, 1, c.tol,
-                                    P(self.pool_beta), P(self.pool_n), P(self.pool_rank)), "pool_solve")
-            mark("pooled_ols", 1)
-        if on("predict"):
-            mark("predict", 0)
-            chk(L.afm_predict_f64(h, P(self.out), T * lda, lda, self.t_test, T - self.t_test,
-                                  P(self.cols), p, P(self.pool_beta), 0, P(self.finite), c.ycol,
-                                  P(self.pred)), "predict")
-            mark("predict", 1)
-        if on("rebalance"):
-            mark("rebalance", 0)
-            r = self.reb
-            chk(L.afm_rebalance_f64(h, T, g.A, lda, P(self.rdates), self.nd, P(self.pred),
-                                    P(g.tbits), P(self.out[c.ycol]), P(g.vbits), 0, T,
-                                    -1 if c.window is None else int(c.window), P(g.close),
-                                    P(self.out[N_FACTORS - 1]), c.top_n, c.lo, c.hi, P(r["k"]),
-                                    P(r["books"]), P(r["weights"]), P(r["sums"]), P(r["upos"]),
-                                    P(r["usize"]), P(r["status"])), "rebalance")
-            mark("rebalance", 1)
-        if on("pnl"):
-            mark("pnl", 0)
-            r = self.reb
-            q = self.pnl
-            chk(L.afm_pnl_scan_f64(h, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]), P(r["upos"]),
-                                   P(r["usize"]), 100000000.0, c.rate, P(q["value"]),
-                                   P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])), "pnl")
-            mark("pnl", 1)
-        if joined is not None:
-            joined.wait_stream(self.side)                 # the step ends when both are done
+            if on("factors"):
+                mark("factors", 0)
+                # label planes (target, tmr_ret1d) on the side stream, next to the factor kernel
+                with torch.cuda.stream(self.side):
+                    hs = self.ctx.bind_stream()
+                    chk(L.afm_labels_f64(hs, T, lda, 0, T, P(g.excess), P(g.ret1d), P(g.vbits),
+                                         P(self.out[TARGET]), P(self.out[TMR])),
+                        "labels")
+                h = self.ctx.bind_stream()
+                chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), None, None,
+                                      P(g.vbits), P(self.out), P(self.nanfree), P(self.finite)),
+                    "factors")
+                chk(L.afm_drop_last_obs_bits(h, T, lda, P(g.vbits), P(self.finite), P(self.rows)),
+                    "label rows")
+                self.main.wait_stream(self.side)            # the Gram reads the target plane
+                mark("factors", 1)
+            tt = self.t_test
+            if on("xs_gram"):                                  # train + valid dates
+                mark("xs_gram", 0)
+                chk(L.afm_xs_gram_f64(h, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p,
+                                      c.ycol, P(self.rows), 0, tt, P(self.gram), P(self.shift)),
+                    "xs_gram")
+                mark("xs_gram", 1)
+            if on("xs_solve") or on("xs_gram_test"):
+                self.side.wait_stream(self.main)               # after the train+valid Grams
+                with torch.cuda.stream(self.side):
+                    hs = self.ctx.bind_stream()
+                    mark("xs_gram_test", 0)                    # test dates
+                    chk(L.afm_xs_gram_f64(hs, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p,
+                                          c.ycol, P(self.rows), tt, T - tt, P(self.gram[tt:]),
+                                          P(self.shift[tt:])), "xs_gram_test")
+                    mark("xs_gram_test", 1)
+                    if on("xs_solve"):
+                        mark("xs_solve", 0)
+                        chk(L.afm_ols_solve_f64(hs, P(self.gram), P(self.shift), p, T, c.tol,
+                                                P(self.beta), P(self.nobs), P(self.rank)),
+                            "ols_solve")
+                        chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1,
+                                                   P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
+                        mark("xs_solve", 1)
+                h = self.ctx.bind_stream()
+            if on("pooled_ols"):
+                mark("pooled_ols", 0)
+                chk(L.afm_pool_moments_f64(h, P(self.gram), P(self.shift), p, self.t_test,
+                                           P(self.pool_g), P(self.pool_s)), "pool")
+                chk(L.afm_ols_solve_f64(h, P(self.pool_g), P(self.pool_s), p, 1, c.tol,
+                                        P(self.pool_beta), P(self.pool_n), P(self.pool_rank)),
+                    "pool_solve")
+                mark("pooled_ols", 1)
+            if on("predict"):
+                mark("predict", 0)
+                chk(L.afm_predict_f64(h, P(self.out), T * lda, lda, self.t_test, T - self.t_test,
+                                      P(self.cols), p, P(self.pool_beta), 0, P(self.finite),
+                                      c.ycol, P(self.pred)), "predict")
+                mark("predict", 1)
+            if on("rebalance"):
+                mark("rebalance", 0)
+                r = self.reb
+                chk(L.afm_rebalance_f64(h, T, g.A, lda, P(self.rdates), self.nd, P(self.pred),
+                                        P(g.tbits), P(self.out[c.ycol]), P(g.vbits), 0, T,
+                                        -1 if c.window is None else int(c.window), P(g.close),
+                                        P(self.out[N_FACTORS - 1]), c.top_n, c.lo, c.hi,
+                                        P(r["k"]), P(r["books"]), P(r["weights"]), P(r["sums"]),
+                                        P(r["upos"]), P(r["usize"]), P(r["status"])), "rebalance")
+                mark("rebalance", 1)
+            if on("pnl"):
+                mark("pnl", 0)
+                r = self.reb
+                q = self.pnl
+                chk(L.afm_pnl_scan_f64(h, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]),
+                                       P(r["upos"]), P(r["usize"]), 100000000.0, c.rate,
+                                       P(q["value"]), P(q["turnover"]), P(q["long_ret"]),
+                                       P(q["short_ret"])), "pnl")
+                mark("pnl", 1)
+        caller.wait_stream(self.main)                      # the step ends when both are done
+        caller.wait_stream(self.side)
+        self.ctx.bind_stream()
 
     def summary(self) -> dict:
         """Host copies of the headline results (after a synchronize)."""

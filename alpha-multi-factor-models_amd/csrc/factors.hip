@@ -1150,8 +1150,9 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     AFM_CTX(ctx);
     AFM_CHECK_ARG(T > 0 && A > 0, "T and A must be positive");
     AFM_CHECK_ARG(lda >= A && lda % 64 == 0, "lda must be a multiple of 64 and >= A");
-    AFM_CHECK_ARG(close && volume && ret1d && excess && valid_bits && out && nanfree_bits,
-                  "null buffer");
+    AFM_CHECK_ARG(close && volume && valid_bits && out && nanfree_bits, "null buffer");
+    AFM_CHECK_ARG((ret1d == nullptr) == (excess == nullptr),
+                  "ret1d and excess are both given or both NULL");
     AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
     const int64_t nwords = (T + 63) / 64;
     const int64_t nblk = (A + 63) / 64;
@@ -1232,10 +1233,12 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                        ctx->stream, nwords, lda, types, valid_bits, part, part + types * nw,
                        nanfree_bits, finite_bits);
     AFM_HIP(hipGetLastError());
-    dim3 g2((unsigned)(lda / 64), (unsigned)((T + 3) / 4));
-    hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, (int64_t)0, T, lda,
-                       excess, ret1d, valid_bits, out + 96 * a.plane, out + 97 * a.plane);
-    AFM_HIP(hipGetLastError());
+    if (excess) {                  // NULL: the caller runs afm_labels_f64 (e.g. on another stream)
+        dim3 g2((unsigned)(lda / 64), (unsigned)((T + 3) / 4));
+        hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, (int64_t)0, T,
+                           lda, excess, ret1d, valid_bits, out + 96 * a.plane, out + 97 * a.plane);
+        AFM_HIP(hipGetLastError());
+    }
     AFM_HIP(hipFreeAsync(part, ctx->stream));
     return AFM_OK;
 }

@@ -775,15 +775,17 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
 // per = 64 give the same tree for any split of the segments into 64-aligned shards (multi-GPU).
 constexpr int kPoolBlock = 64;
 
-// Each thread owns up to kPoolPer elements of the lower triangle (its centered sums live in
-// registers); the next segment's Gram entries are prefetched while the current one is merged, so
-// the per-block chain runs at two barriers per segment instead of global-load latency.
-constexpr int kPoolPer = ((kMaxF - 1) * kMaxF / 2 + kThreads - 1) / kThreads;
+// The lower triangle is split over gridDim.y workgroups per date block (kPoolPer elements per
+// thread each): every element's chain of merges is independent of the others, so the split only
+// shortens each thread's per-segment work (one division per element) and leaves every result
+// bit-identical.  The merge scalars (n, Chan factor, means) are recomputed by each workgroup of
+// the split.  The next segment's entries are prefetched while the current one is merged (two
+// barriers per segment).
+constexpr int kPoolPer = 4;
 
 __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, const double* shift,
                                                         int p2, int64_t nseg, int64_t per,
                                                         double* out_gram, double* out_shift) {
-    extern __shared__ __attribute__((aligned(16))) double C[];   // [p2][p2] (epilogue only)
     __shared__ double mu[kMaxF];
     __shared__ double dl[kMaxF];
     __shared__ double g0[kMaxF];
@@ -794,11 +796,12 @@ __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, cons
     const int nel = q * (q + 1) / 2;
     const int64_t s0 = (int64_t)blockIdx.x * per;
     const int64_t s1 = s0 + per < nseg ? s0 + per : nseg;
-    // my elements: e = tid + k * kThreads -> (r, c), 1 <= c <= r <= q
+    const int ebase = (int)blockIdx.y * kPoolPer * kThreads;
+    // my elements: e = ebase + tid + k * kThreads -> (r, c), 1 <= c <= r <= q
     int ro[kPoolPer], co[kPoolPer];
 #pragma unroll
     for (int k = 0; k < kPoolPer; ++k) {
-        const int e = tid + k * kThreads;
+        const int e = ebase + tid + k * kThreads;
         int r = (int)((__builtin_sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
         while ((r + 1) * (r + 2) / 2 <= e) ++r;
         while (r * (r + 1) / 2 > e) --r;
@@ -853,20 +856,28 @@ __global__ __launch_bounds__(kThreads) void pool_kernel(const double* gram, cons
         scur = snxt;
         ncur = nnxt;
     }
-    // (the last mu update and the accumulators are published through LDS)
+    __syncthreads();                                   // the last mu update
+    double* og = out_gram + (int64_t)blockIdx.x * q2;
 #pragma unroll
     for (int k = 0; k < kPoolPer; ++k)
-        if (tid + k * kThreads < nel) C[ro[k] * p2 + co[k]] = acc[k];
-    __syncthreads();
-    double* og = out_gram + (int64_t)blockIdx.x * q2;
-    const int ty = tid >> 4, tx = tid & 15;
-    for (int r = ty; r < p2; r += 16)
-        for (int c = tx; c < p2; c += 16) {
-            const double v = (r == 0 && c == 0) ? ntot_s
-                             : ((r == 0 || c == 0) ? 0.0 : (c <= r ? C[r * p2 + c] : C[c * p2 + r]));
-            og[r * p2 + c] = v;
+        if (ebase + tid + k * kThreads < nel) {
+            og[ro[k] * p2 + co[k]] = acc[k];
+            og[co[k] * p2 + ro[k]] = acc[k];
         }
-    if (tid < p2) out_shift[(int64_t)blockIdx.x * p2 + tid] = (tid == 0) ? 0.0 : mu[tid];
+    if (blockIdx.y == 0) {                             // row / column 0: n, zeros; the means
+        const double ntot = ntot_s;
+        for (int c = tid; c < p2; c += kThreads) {
+            og[c] = c == 0 ? ntot : 0.0;
+            if (c > 0) og[c * p2] = 0.0;
+        }
+        if (tid < p2) out_shift[(int64_t)blockIdx.x * p2 + tid] = (tid == 0) ? 0.0 : mu[tid];
+    }
+}
+
+// workgroups per date block that split the lower triangle of a (p2 x p2) Gram
+static unsigned pool_split(int p2) {
+    const int nel = (p2 - 1) * p2 / 2;
+    return (unsigned)((nel + kPoolPer * kThreads - 1) / (kPoolPer * kThreads));
 }
 
 // ---- predictions: pred[t][a] = beta0 + sum_j beta_j x_j (grid rows with a set mask bit) ------
@@ -1051,12 +1062,10 @@ extern "C" int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const doub
     AFM_CHECK_ARG(p >= 1 && p + 2 <= kMaxF, "need 1 <= p <= 110");
     AFM_CHECK_ARG(gram && shift && out_gram && out_shift && nseg >= 0, "bad arguments");
     const int p2 = p + 2;
-    const size_t lds = sizeof(double) * p2 * p2;
-    AFM_HIP(hipFuncSetAttribute((const void*)pool_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const unsigned ny = pool_split(p2);
     const int64_t nb = (nseg + kPoolBlock - 1) / kPoolBlock;
     if (nb <= 1) {
-        hipLaunchKernelGGL(pool_kernel, dim3(1), dim3(kThreads), lds, ctx->stream, gram, shift,
+        hipLaunchKernelGGL(pool_kernel, dim3(1, ny), dim3(kThreads), 0, ctx->stream, gram, shift,
                            p2, nseg, (int64_t)kPoolBlock, out_gram, out_shift);
         AFM_HIP(hipGetLastError());
         return AFM_OK;
@@ -1065,10 +1074,10 @@ extern "C" int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const doub
     AFM_HIP(hipMallocAsync((void**)&work, sizeof(double) * nb * (p2 * p2 + p2), ctx->stream));
     double* wg = work;
     double* ws = work + nb * p2 * p2;
-    hipLaunchKernelGGL(pool_kernel, dim3((unsigned)nb), dim3(kThreads), lds, ctx->stream, gram,
+    hipLaunchKernelGGL(pool_kernel, dim3((unsigned)nb, ny), dim3(kThreads), 0, ctx->stream, gram,
                        shift, p2, nseg, (int64_t)kPoolBlock, wg, ws);
     AFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(pool_kernel, dim3(1), dim3(kThreads), lds, ctx->stream, wg, ws, p2, nb, nb,
+    hipLaunchKernelGGL(pool_kernel, dim3(1, ny), dim3(kThreads), 0, ctx->stream, wg, ws, p2, nb, nb,
                        out_gram, out_shift);
     AFM_HIP(hipGetLastError());
     AFM_HIP(hipFreeAsync(work, ctx->stream));
@@ -1083,12 +1092,9 @@ extern "C" int afm_pool_segments_f64(afm_ctx* ctx, const double* gram, const dou
     AFM_CHECK_ARG(gram && shift && out_gram && out_shift && nseg >= 0 && per >= 1, "bad arguments");
     if (nseg == 0) return AFM_OK;
     const int p2 = p + 2;
-    const size_t lds = sizeof(double) * p2 * p2;
-    AFM_HIP(hipFuncSetAttribute((const void*)pool_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t nb = (nseg + per - 1) / per;
-    hipLaunchKernelGGL(pool_kernel, dim3((unsigned)nb), dim3(kThreads), lds, ctx->stream, gram,
-                       shift, p2, nseg, per, out_gram, out_shift);
+    hipLaunchKernelGGL(pool_kernel, dim3((unsigned)nb, pool_split(p2)), dim3(kThreads), 0,
+                       ctx->stream, gram, shift, p2, nseg, per, out_gram, out_shift);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
