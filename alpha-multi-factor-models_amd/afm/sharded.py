@@ -210,6 +210,9 @@ class ShardedPipeline:
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         self.ctx = _lib.Context.get(dev.index)
+        # side stream: the full-width label planes (next to the factor kernel) and the per-date
+        # solve of the owned dates (nothing on the main chain reads the betas)
+        self.side = torch.cuda.Stream(device=dev)
 
     def n_asset_days_local(self) -> int:
         return int(self.loc.valid.sum().item())
@@ -231,15 +234,23 @@ class ShardedPipeline:
                 events[stage][which].record()
 
         g = self.loc
+        f = self.full
+        main = torch.cuda.current_stream(self.out.device)
+        side = self.side
+        side.wait_stream(main)
         mark("factors", 0)
+        with torch.cuda.stream(side):                 # history label planes, all assets
+            hs = self.ctx.bind_stream()
+            chk(L.afm_labels_f64(hs, T, lda, self.lab0, T, P(f.excess), P(f.ret1d), P(f.vbits),
+                                 P(self.target), P(self.tmr)), "labels")
+            labels_done = torch.cuda.Event()
+            labels_done.record(side)
+        h = self.ctx.bind_stream()
         chk(L.afm_factors_f64(h, T, self.A_r, lr, P(g.close), P(g.volume), P(g.ret1d),
                               P(g.excess), P(g.vbits), P(self.out), P(self.nanfree),
                               P(self.finite)), "factors")
         chk(L.afm_drop_last_obs_bits(h, T, lr, P(g.vbits), P(self.finite), P(self.rows)),
             "label rows")
-        f = self.full
-        chk(L.afm_labels_f64(h, T, lda, self.lab0, T, P(f.excess), P(f.ret1d), P(f.vbits),
-                             P(self.target), P(self.tmr)), "labels")
         mark("factors", 1)
         mark("xs_gram", 0)
         chk(L.afm_xs_gram_f64(h, P(self.out), T * lr, lr, self.A_r, -1, P(self.cols), p, c.ycol,
@@ -257,24 +268,23 @@ class ShardedPipeline:
         rg[:, self.tri_t] = recv[:, :self.ntri]
         mark("exchange", 1)
         h = self.ctx.bind_stream()
-        mark("xs_solve", 0)
         if self.nd_own > 0:
             rg = rg.view(W, self.nd_own, p2 * p2).transpose(0, 1).contiguous()   # [date][rank]
             rs = rs.view(W, self.nd_own, p2).transpose(0, 1).contiguous()
             chk(L.afm_pool_segments_f64(h, P(rg), P(rs), p, self.nd_own * W, W, P(self.gram),
                                         P(self.shift)), "merge partial moments")
-            chk(L.afm_ols_solve_f64(h, P(self.gram), P(self.shift), p, self.nd_own, c.tol,
-                                    P(self.beta_own), P(self.nobs_own), P(self.rank_own)),
-                "ols_solve")
-        bg, ng, kg = cm.all_gather_packed([self.beta_own, self.nobs_own, self.rank_own])
-        for q, (lo, hi) in enumerate(self.drange):
-            self.beta[lo:hi] = bg[q, :hi - lo]
-            self.nobs[lo:hi] = ng[q, :hi - lo]
-            self.rank[lo:hi] = kg[q, :hi - lo]
+        # per-date solve of the owned dates on the side stream; its beta all-gather + Fama-MacBeth
+        # are issued after the main chain's collectives (one RCCL stream serialises collectives
+        # in issue order, so issuing it here would hold the pooled-OLS gather behind the solve)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            hs = self.ctx.bind_stream()
+            mark("xs_solve", 0)
+            if self.nd_own > 0:
+                chk(L.afm_ols_solve_f64(hs, P(self.gram), P(self.shift), p, self.nd_own, c.tol,
+                                        P(self.beta_own), P(self.nobs_own), P(self.rank_own)),
+                    "ols_solve")
         h = self.ctx.bind_stream()
-        chk(L.afm_fama_macbeth_f64(h, P(self.beta), P(self.rank), T, p + 1, P(self.fm_mean),
-                                   P(self.fm_t)), "fama_macbeth")
-        mark("xs_solve", 1)
         # ---- pooled OLS over [0, t_test): owned 64-date blocks, gathered in date order ----
         mark("pooled_ols", 0)
         ntr = self.ntr_q[cm.rank]
@@ -307,6 +317,7 @@ class ShardedPipeline:
             self.pred[self.t_test:, lo:lo + self.lda_q[q]] = pg[q, :, :self.lda_q[q]]
         mark("predict", 1)
         # ---- rebalance + KKT on the owned rebalance dates (+ one neighbour per side) ----
+        main.wait_event(labels_done)                   # history planes
         h = self.ctx.bind_stream()
         mark("rebalance", 0)
         x = self.reb_ext
@@ -339,6 +350,19 @@ class ShardedPipeline:
                                P(r["usize"]), 100000000.0, c.rate, P(q_["value"]),
                                P(q_["turnover"]), P(q_["long_ret"]), P(q_["short_ret"])), "pnl")
         mark("pnl", 1)
+        # ---- per-date betas -> every rank, Fama-MacBeth (side stream, overlaps the PnL scan) ----
+        with torch.cuda.stream(side):
+            bg, ng, kg = cm.all_gather_packed([self.beta_own, self.nobs_own, self.rank_own])
+            for q, (lo, hi) in enumerate(self.drange):
+                self.beta[lo:hi] = bg[q, :hi - lo]
+                self.nobs[lo:hi] = ng[q, :hi - lo]
+                self.rank[lo:hi] = kg[q, :hi - lo]
+            hs = self.ctx.bind_stream()
+            chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1, P(self.fm_mean),
+                                       P(self.fm_t)), "fama_macbeth")
+            mark("xs_solve", 1)
+        main.wait_stream(side)                         # the step ends when both are done
+        self.ctx.bind_stream()
 
     def summary(self) -> dict:
         v = self.pnl["value"].cpu().numpy()
