@@ -26,7 +26,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from .factors import N_FACTORS, TARGET, TMR
+from .factors import N_FACTORS, TARGET
 from .grid import PanelGrid
 from .portfolio import MAX_BOOK
 
@@ -100,10 +100,10 @@ class Pipeline:
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         self.ctx = _lib.Context.get(dev.index)
-        # the step's latency-critical chain runs on a high-priority stream; the label planes
-        # (next to the factor kernel) and the test dates' Grams + per-date solve + Fama-MacBeth
-        # (results nobody downstream reads) run on a low-priority side stream, so the queue
-        # arbiter hands freed CU slots to the main chain first (AFM_PIPE_PRIO=0: equal priority)
+        # the step's latency-critical chain runs on a high-priority stream; the test dates'
+        # Grams + per-date solve + Fama-MacBeth (results nobody downstream reads) run on a
+        # low-priority side stream, so the queue arbiter hands freed CU slots to the main chain
+        # first (AFM_PIPE_PRIO=0: equal priority)
         import os
         prio = os.environ.get("AFM_PIPE_PRIO", "1") != "0"
         self.main = torch.cuda.Stream(device=dev, priority=-8 if prio else 0)
@@ -134,19 +134,14 @@ class Pipeline:
             h = self.ctx.bind_stream()
             if on("factors"):
                 mark("factors", 0)
-                # label planes (target, tmr_ret1d) on the side stream, next to the factor kernel
-                with torch.cuda.stream(self.side):
-                    hs = self.ctx.bind_stream()
-                    chk(L.afm_labels_f64(hs, T, lda, 0, T, P(g.excess), P(g.ret1d), P(g.vbits),
-                                         P(self.out[TARGET]), P(self.out[TMR])),
-                        "labels")
-                h = self.ctx.bind_stream()
-                chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), None, None,
-                                      P(g.vbits), P(self.out), P(self.nanfree), P(self.finite)),
-                    "factors")
+                # (label planes in the same call: on a side stream next to the latency-bound
+                # factor kernel they slowed it by more than their own time -- A/B on MI355X,
+                # 2500-asset shard 5.5 -> 7.1 ms -- and the Grams read the target plane)
+                chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), P(g.ret1d),
+                                      P(g.excess), P(g.vbits), P(self.out), P(self.nanfree),
+                                      P(self.finite)), "factors")
                 chk(L.afm_drop_last_obs_bits(h, T, lda, P(g.vbits), P(self.finite), P(self.rows)),
                     "label rows")
-                self.main.wait_stream(self.side)            # the Gram reads the target plane
                 mark("factors", 1)
             tt = self.t_test
             if on("xs_gram"):                                  # train + valid dates

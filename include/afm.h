@@ -55,8 +55,7 @@ const char* afm_factor_name(int i);
  * finite_bits (optional, may be NULL): present AND all 96 factor columns finite (dropna keeps
  * +-inf, e.g. vol_change after a zero-volume day; the regression stages need finite rows).
  * ret1d and excess may both be NULL: the label planes 96-97 are then not written, and the caller
- * fills them with afm_labels_f64 (the pipeline runs it on a second stream, next to the factor
- * kernel). */
+ * fills them with afm_labels_f64 (e.g. on another stream, or for another asset range). */
 int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                     const double* close, const double* volume, const double* ret1d,
                     const double* excess, const uint64_t* valid_bits,
