@@ -31,6 +31,7 @@ SIGNATURES = {
     "afm_xs_gram_f64": (I32, [P, P, I64, I64, I64, I64, P, I32, I32, P, I64, I64, P, P]),
     "afm_ols_solve_f64": (I32, [P, P, P, I32, I64, DBL, P, P, P]),
     "afm_pool_moments_f64": (I32, [P, P, P, I32, I64, P, P]),
+    "afm_pool_tree_f64": (I32, [P, P, P, I32, I64, I32, P, P]),
     "afm_pool_segments_f64": (I32, [P, P, P, I32, I64, I64, P, P]),
     "afm_labels_f64": (I32, [P, I64, I64, I64, I64, P, P, P, P, P]),
     "afm_drop_last_obs_bits": (I32, [P, I64, I64, P, P, P]),

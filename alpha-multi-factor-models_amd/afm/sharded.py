@@ -172,6 +172,12 @@ class ShardedPipeline:
         self.nb_max = max(max(self.nb_q), 1)
         self.blk_g = torch.zeros((self.nb_max, p2, p2), **f64)
         self.blk_s = torch.zeros((self.nb_max, p2), **f64)
+        self.blk16_g = torch.zeros((4 * self.nb_max, p2, p2), **f64)     # tree level 0 results
+        self.blk16_s = torch.zeros((4 * self.nb_max, p2), **f64)
+        # the gathered [W][nb_max] blocks without the padding: the 64-date blocks in date order
+        self.blk_idx = torch.as_tensor(np.concatenate(
+            [q * self.nb_max + np.arange(self.nb_q[q]) for q in range(W)]).astype(np.int64),
+            device=dev)
         self.pool_g = torch.empty((1, p2, p2), **f64)
         self.pool_s = torch.empty((1, p2), **f64)
         self.pool_beta = torch.empty((1, p + 1), **f64)
@@ -289,20 +295,24 @@ class ShardedPipeline:
                                         P(self.beta_own), P(self.nobs_own), P(self.rank_own)),
                     "ols_solve")
         h = self.ctx.bind_stream()
-        # ---- pooled OLS over [0, t_test): owned 64-date blocks, gathered in date order ----
+        # ---- pooled OLS over [0, t_test): owned 64-date blocks, gathered in date order, then the
+        # rest of afm_pool_moments_f64's tree (the same tree as one device: bit-identical) ----
         mark("pooled_ols", 0)
         ntr = self.ntr_q[cm.rank]
         self.blk_g.zero_()
         self.blk_s.zero_()
-        if ntr > 0:
-            chk(L.afm_pool_segments_f64(h, P(self.gram), P(self.shift), p, ntr, 64,
-                                        P(self.blk_g), P(self.blk_s)), "pool blocks")
+        if ntr > 0:                                   # tree levels 0-1 (afm_pool_tree_f64)
+            n16 = (ntr + 15) // 16
+            chk(L.afm_pool_segments_f64(h, P(self.gram), P(self.shift), p, ntr, 16,
+                                        P(self.blk16_g), P(self.blk16_s)), "pool 16-date blocks")
+            chk(L.afm_pool_segments_f64(h, P(self.blk16_g), P(self.blk16_s), p, n16, 4,
+                                        P(self.blk_g), P(self.blk_s)), "pool 64-date blocks")
         ag, as_ = cm.all_gather_packed([self.blk_g, self.blk_s])
-        ag = ag.reshape(W * self.nb_max, p2, p2).contiguous()
-        as_ = as_.reshape(W * self.nb_max, p2).contiguous()
+        ag = ag.reshape(W * self.nb_max, p2, p2).index_select(0, self.blk_idx).contiguous()
+        as_ = as_.reshape(W * self.nb_max, p2).index_select(0, self.blk_idx).contiguous()
         h = self.ctx.bind_stream()
-        chk(L.afm_pool_segments_f64(h, P(ag), P(as_), p, W * self.nb_max, W * self.nb_max,
-                                    P(self.pool_g), P(self.pool_s)), "pool")
+        chk(L.afm_pool_tree_f64(h, P(ag), P(as_), p, int(self.blk_idx.numel()), 2,
+                                P(self.pool_g), P(self.pool_s)), "pool")
         chk(L.afm_ols_solve_f64(h, P(self.pool_g), P(self.pool_s), p, 1, c.tol,
                                 P(self.pool_beta), P(self.pool_n), P(self.pool_rank)),
             "pool_solve")

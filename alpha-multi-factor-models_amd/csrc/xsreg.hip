@@ -771,9 +771,9 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
 // ---- exact (Chan) combination of per-segment shifted moments ----------------------------------
 // Block b combines segments [b*per, min((b+1)*per, nseg)) in order and emits the union's moments
 // in the same "shifted" representation (G'[0][0] = n, G'[0][j] = 0, G'[i][j] = centered sums,
-// shift = mean), so a second pass (or ols_solve_kernel) consumes it unchanged.  Two passes with
-// per = 64 give the same tree for any split of the segments into 64-aligned shards (multi-GPU).
-constexpr int kPoolBlock = 64;
+// shift = mean), so a next level (or ols_solve_kernel) consumes it unchanged.  pool_tree below
+// fixes the tree (16, 4, then 8 per level): the same for any split of the segments into
+// 64-aligned shards (multi-GPU).
 
 // The lower triangle is split over gridDim.y workgroups per date block (kPoolPer elements per
 // thread each): every element's chain of merges is independent of the others, so the split only
@@ -1056,32 +1056,61 @@ extern "C" int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double*
     return AFM_OK;
 }
 
+// The pooling tree: level 0 merges 16 consecutive segments (dates), level 1 four level-0
+// results (64-date blocks), every later level 8 results, until one is left.  Each level is one
+// pool_kernel launch whose chains are at most 16 merges long (the former two-pass tree ran 64 +
+// 63 sequential merges).  The tree is a fixed function of the segment list, so any split of the
+// dates into 64-aligned ranges (multi-GPU) reproduces it: a rank pools its own dates through
+// levels 0-1 and the gathered 64-date blocks go through levels 2+ (afm_pool_tree_f64).
+static int64_t pool_level_per(int level) { return level == 0 ? 16 : level == 1 ? 4 : 8; }
+
+static int pool_tree(afm_ctx* ctx, const double* gram, const double* shift, int p, int64_t nseg,
+                     int level0, double* out_gram, double* out_shift) {
+    const int p2 = p + 2;
+    const unsigned ny = pool_split(p2);
+    // (a level over one segment is an exact identity merge: from n = 0 the Chan factor is 0)
+    auto blocks = [](int64_t n, int64_t per) -> int64_t { return n <= per ? 1 : (n + per - 1) / per; };
+    const int64_t nb0 = blocks(nseg, pool_level_per(level0));
+    double* work = nullptr;
+    if (nb0 > 1) {
+        AFM_HIP(hipMallocAsync((void**)&work, sizeof(double) * 2 * nb0 * (p2 * p2 + p2),
+                               ctx->stream));
+    }
+    const double* ig = gram;
+    const double* is = shift;
+    int64_t n = nseg;
+    for (int level = level0, pp = 0;; ++level, pp ^= 1) {
+        const int64_t per = pool_level_per(level);
+        const int64_t nb = blocks(n, per);
+        double* og = nb == 1 ? out_gram : work + pp * nb0 * (p2 * p2 + p2);
+        double* os = nb == 1 ? out_shift : og + nb0 * p2 * p2;
+        hipLaunchKernelGGL(pool_kernel, dim3((unsigned)nb, ny), dim3(kThreads), 0, ctx->stream, ig,
+                           is, p2, n, per, og, os);
+        AFM_HIP(hipGetLastError());
+        if (nb == 1) break;
+        ig = og;
+        is = os;
+        n = nb;
+    }
+    if (work) AFM_HIP(hipFreeAsync(work, ctx->stream));
+    return AFM_OK;
+}
+
 extern "C" int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
                                     int64_t nseg, double* out_gram, double* out_shift) {
     AFM_CTX(ctx);
     AFM_CHECK_ARG(p >= 1 && p + 2 <= kMaxF, "need 1 <= p <= 110");
     AFM_CHECK_ARG(gram && shift && out_gram && out_shift && nseg >= 0, "bad arguments");
-    const int p2 = p + 2;
-    const unsigned ny = pool_split(p2);
-    const int64_t nb = (nseg + kPoolBlock - 1) / kPoolBlock;
-    if (nb <= 1) {
-        hipLaunchKernelGGL(pool_kernel, dim3(1, ny), dim3(kThreads), 0, ctx->stream, gram, shift,
-                           p2, nseg, (int64_t)kPoolBlock, out_gram, out_shift);
-        AFM_HIP(hipGetLastError());
-        return AFM_OK;
-    }
-    double* work = nullptr;
-    AFM_HIP(hipMallocAsync((void**)&work, sizeof(double) * nb * (p2 * p2 + p2), ctx->stream));
-    double* wg = work;
-    double* ws = work + nb * p2 * p2;
-    hipLaunchKernelGGL(pool_kernel, dim3((unsigned)nb, ny), dim3(kThreads), 0, ctx->stream, gram,
-                       shift, p2, nseg, (int64_t)kPoolBlock, wg, ws);
-    AFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(pool_kernel, dim3(1, ny), dim3(kThreads), 0, ctx->stream, wg, ws, p2, nb, nb,
-                       out_gram, out_shift);
-    AFM_HIP(hipGetLastError());
-    AFM_HIP(hipFreeAsync(work, ctx->stream));
-    return AFM_OK;
+    return pool_tree(ctx, gram, shift, p, nseg, 0, out_gram, out_shift);
+}
+
+extern "C" int afm_pool_tree_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
+                                 int64_t nseg, int level0, double* out_gram, double* out_shift) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(p >= 1 && p + 2 <= kMaxF, "need 1 <= p <= 110");
+    AFM_CHECK_ARG(gram && shift && out_gram && out_shift && nseg >= 0 && level0 >= 0,
+                  "bad arguments");
+    return pool_tree(ctx, gram, shift, p, nseg, level0, out_gram, out_shift);
 }
 
 extern "C" int afm_pool_segments_f64(afm_ctx* ctx, const double* gram, const double* shift,

@@ -96,9 +96,15 @@ int afm_pool_moments_f64(afm_ctx* ctx, const double* gram, const double* shift, 
                          int64_t nseg, double* out_gram, double* out_shift);
 /* Segmented version: out[b] combines segments [b*per, min((b+1)*per, nseg)) in order (Chan), for
  * b < ceil(nseg/per) -- e.g. the per-rank partial moments of one date (multi-GPU asset shards), or
- * the 64-date blocks of afm_pool_moments_f64's first pass.  Segments with n = 0 are skipped. */
+ * one level of afm_pool_moments_f64's tree.  Segments with n = 0 are skipped. */
 int afm_pool_segments_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
                           int64_t nseg, int64_t per, double* out_gram, double* out_shift);
+/* afm_pool_moments_f64's fixed tree (level 0 merges 16 segments, level 1 four level-0 results =
+ * 64-date blocks, later levels 8 results each, until one remains) entered at level level0: the
+ * multi-GPU step pools each rank's dates through levels 0-1 (afm_pool_segments_f64 with per 16,
+ * then 4) and the gathered 64-date blocks with level0 = 2 -- the same tree as one device. */
+int afm_pool_tree_f64(afm_ctx* ctx, const double* gram, const double* shift, int p, int64_t nseg,
+                      int level0, double* out_gram, double* out_shift);
 /* pred[t][a] = beta[t-t0][0] + sum_j beta[t-t0][1+j] * x_cols[j][t][a] on grid rows with a mask
  * bit (NaN elsewhere), t in [t0, t0+nt); beta_stride = 0 applies one coefficient vector.
  * ycheck >= 0: additionally require column ycheck finite (e.g. the label of a dropna'd row). */

@@ -159,3 +159,69 @@ def test_linear_regression_dropin_matches_reference(golden_dir):
     mf = LinearRegression().fit(Xf, ytr["target"].to_numpy())
     pf = mf.predict(parts["te"][0])
     assert np.abs(pf - o["full_pred"]).max() / np.abs(o["full_pred"]).max() < 1e-6
+
+
+@pytest.mark.parametrize("p,nseg,cut", [(96, 4032, 2048), (7, 700, 320), (30, 50, 0), (5, 1, 0)])
+def test_pool_tree_split_identical(p, nseg, cut):
+    """afm_pool_moments_f64's fixed tree == the multi-GPU composition (each 64-aligned date range
+    through levels 0-1 with afm_pool_segments_f64 per 16 then 4, the 64-date blocks of both ranges
+    through afm_pool_tree_f64 from level 2): bit-identical; and the pooled moments match the
+    exact centered sums of all segments (rel 1e-12)."""
+    import torch
+    from afm import _lib
+    L, P = _lib.lib(), _lib.ptr
+    rng = np.random.default_rng(nseg + p)
+    p2 = p + 2
+    dev = torch.device("cuda:0")
+    # per-segment shifted moments of random rows: G = [n, sum(z - s); ..., sum (z-s)(z-s)']
+    n = rng.integers(0, 40, size=nseg).astype(np.float64)
+    n[rng.random(nseg) < 0.05] = 0                       # empty segments are skipped
+    G = np.zeros((nseg, p2, p2))
+    S = np.zeros((nseg, p2))
+    allz = []
+    for k in range(nseg):
+        z = rng.normal(3.0, 2.0, size=(int(n[k]), p + 1))
+        allz.append(z)
+        s = z[0] if len(z) else np.zeros(p + 1)
+        d = z - s
+        G[k, 0, 0] = n[k]
+        G[k, 0, 1:] = G[k, 1:, 0] = d.sum(axis=0)
+        G[k, 1:, 1:] = d.T @ d
+        S[k, 1:] = s
+    g = torch.from_numpy(G).to(dev)
+    sh = torch.from_numpy(S).to(dev)
+    ctx = _lib.Context.get(0)
+    h = ctx.bind_stream()
+    og = torch.empty((1, p2, p2), dtype=torch.float64, device=dev)
+    osh = torch.empty((1, p2), dtype=torch.float64, device=dev)
+    _lib.check(L.afm_pool_moments_f64(h, P(g), P(sh), p, nseg, P(og), P(osh)), "pool")
+    blocks_g, blocks_s = [], []
+    for lo, hi in ((0, cut), (cut, nseg)):
+        m = hi - lo
+        if m == 0:
+            continue
+        n16, n64 = (m + 15) // 16, (m + 63) // 64
+        g16 = torch.empty((n16, p2, p2), dtype=torch.float64, device=dev)
+        s16 = torch.empty((n16, p2), dtype=torch.float64, device=dev)
+        g64 = torch.empty((n64, p2, p2), dtype=torch.float64, device=dev)
+        s64 = torch.empty((n64, p2), dtype=torch.float64, device=dev)
+        _lib.check(L.afm_pool_segments_f64(h, P(g[lo:hi]), P(sh[lo:hi]), p, m, 16, P(g16),
+                                           P(s16)), "level 0")
+        _lib.check(L.afm_pool_segments_f64(h, P(g16), P(s16), p, n16, 4, P(g64), P(s64)),
+                   "level 1")
+        blocks_g.append(g64)
+        blocks_s.append(s64)
+    bg = torch.cat(blocks_g).contiguous()
+    bs = torch.cat(blocks_s).contiguous()
+    tg = torch.empty_like(og)
+    ts = torch.empty_like(osh)
+    _lib.check(L.afm_pool_tree_f64(h, P(bg), P(bs), p, bg.shape[0], 2, P(tg), P(ts)), "tree")
+    torch.cuda.synchronize()
+    assert torch.equal(og, tg) and torch.equal(osh, ts)
+    z = np.concatenate(allz)
+    mu = z.mean(axis=0)
+    C = (z - mu).T @ (z - mu)
+    got = og[0].cpu().numpy()
+    assert got[0, 0] == len(z)
+    assert np.abs(osh[0, 1:].cpu().numpy() - mu).max() <= 1e-12 * np.abs(mu).max()
+    assert np.abs(got[1:, 1:] - C).max() <= 1e-12 * np.abs(C).max()
