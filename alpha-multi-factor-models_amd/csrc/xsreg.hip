@@ -674,8 +674,9 @@ __global__ __launch_bounds__(512, 1) void gram_kernel(GramArgs g) {
 // below tol drops its regressor (beta = 0).  The factor is kept unscaled -- the update is
 // M[i][j] -= M[i][k] M[j][k] / d_k -- so each column costs ONE barrier; back substitution
 // beta_j = (M[y][j] - sum_{i>j} M[i][j] beta_i) / d_j runs in one wave.  beta = D b,
-// intercept = ybar - xbar . beta.  One workgroup per segment, the matrix in LDS (76 KB at
-// p = 96: two workgroups per CU).
+// intercept = ybar - xbar . beta.  One workgroup per segment, the lower triangle packed in LDS
+// (row i at i(i+1)/2: 38 KB at p = 96, so four workgroups share a CU where the square layout's
+// 76 KB allowed two; every access is on or below the diagonal).
 struct SolveArgs {
     const double* gram;      // [nseg][p2][p2]
     const double* shift;     // [nseg][p2]
@@ -689,14 +690,15 @@ struct SolveArgs {
 constexpr int kMaxP = kMaxF - 2;
 
 __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
-    extern __shared__ __attribute__((aligned(16))) double M[];    // [q][ld], lower triangle used
+    extern __shared__ __attribute__((aligned(16))) double M[];    // packed lower triangle
     __shared__ double dsc[kMaxP + 1];
     __shared__ double dk[kMaxP];
     __shared__ double mean[kMaxP + 2];
     __shared__ double bvec[kMaxP];
     __shared__ int drop[kMaxP];
     const int tid = threadIdx.x;
-    const int p = s.p, p2 = p + 2, q = p + 1, ld = q + 1;
+    const int p = s.p, p2 = p + 2, q = p + 1;
+    auto row = [](int i) { return i * (i + 1) / 2; };      // offset of row i
     const double* G = s.gram + (int64_t)blockIdx.x * p2 * p2;
     const double* sf = s.shift + (int64_t)blockIdx.x * p2;
     const double n = G[0];
@@ -714,24 +716,25 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
         if (r < p) drop[r] = !(d > 0);
     }
     __syncthreads();
-    // lower triangle of D C D (row-major, ld = q + 1)
+    // lower triangle of D C D (packed rows)
     for (int r = tid >> 4; r < q; r += kThreads >> 4)
         for (int c = tid & 15; c <= r; c += 16) {
             const double v = G[(r + 1) * p2 + c + 1] - G[r + 1] * G[c + 1] / n;
-            M[r * ld + c] = v * dsc[r] * dsc[c];
+            M[row(r) + c] = v * dsc[r] * dsc[c];
         }
     __syncthreads();
     // right-looking Cholesky of the x block, thresholded; the y row rides along
     const int ty = tid >> 4, tx = tid & 15;
     for (int k = 0; k < p; ++k) {
-        const double d = M[k * ld + k];
+        const double d = M[row(k) + k];
         const bool dr = drop[k] || !(d > s.tol);     // uniform: every thread reads the same
         if (!dr) {
             const double inv = 1.0 / d;
             for (int i = k + 1 + ty; i < q; i += 16) {
-                const double mik = M[i * ld + k] * inv;
+                const int ri = row(i);
+                const double mik = M[ri + k] * inv;
                 for (int j = k + 1 + tx; j <= i; j += 16)
-                    M[i * ld + j] = M[i * ld + j] - mik * M[j * ld + k];
+                    M[ri + j] = M[ri + j] - mik * M[row(j) + k];
             }
         }
         if (tid == 0) { drop[k] = dr ? 1 : 0; dk[k] = d; }
@@ -739,14 +742,14 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
     }
     if (tid < 64) {                                  // back substitution, one wave
         const int lane = tid;
-        double t0 = lane < p ? M[p * ld + lane] : 0.0;
-        double t1 = lane + 64 < p ? M[p * ld + lane + 64] : 0.0;
+        double t0 = lane < p ? M[row(p) + lane] : 0.0;
+        double t1 = lane + 64 < p ? M[row(p) + lane + 64] : 0.0;
         for (int k = p - 1; k >= 0; --k) {
             const double tk = __shfl(k >= 64 ? t1 : t0, k & 63, 64);
             const double bk = drop[k] ? 0.0 : tk / dk[k];
             if (lane == 0) bvec[k] = bk;
-            if (lane < k) t0 = t0 - M[k * ld + lane] * bk;
-            if (lane + 64 < k) t1 = t1 - M[k * ld + lane + 64] * bk;
+            if (lane < k) t0 = t0 - M[row(k) + lane] * bk;
+            if (lane + 64 < k) t1 = t1 - M[row(k) + lane + 64] * bk;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bvec visible to the wave
         double part = 0.0;                           // intercept = ybar - sum xbar_j b_j
@@ -1047,7 +1050,7 @@ extern "C" int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double*
     AFM_CHECK_ARG(gram && shift && beta && nobs && rank, "null buffer");
     if (nseg <= 0) return AFM_OK;
     SolveArgs s{gram, shift, p, tol, beta, nobs, rank};
-    const size_t lds = sizeof(double) * (size_t)(p + 1) * (p + 2);
+    const size_t lds = sizeof(double) * (size_t)(p + 1) * (p + 2) / 2;     // packed triangle
     AFM_HIP(hipFuncSetAttribute((const void*)ols_solve_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(ols_solve_kernel, dim3((unsigned)nseg), dim3(kThreads), lds, ctx->stream,
