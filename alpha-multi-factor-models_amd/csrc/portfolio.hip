@@ -883,7 +883,10 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
     int64_t next = 0;
     if (wave == 1) next = stage(0, 0);
     __syncthreads();
-    double V = v0, Vp = v0;
+    double V = v0;
+    // share counts of the previous date, (V_prev / 2) / price sums: the same quotients the
+    // previous date computed as its new ones, carried instead of divided again
+    double qa = 0.0, qb = 0.0;
     if (wave == 0 && lane == 0) value[0] = v0;
     for (int ch = 0;; ++ch) {
         const int b = ch & 1;
@@ -897,17 +900,18 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
             for (int j = 0; j < c; ++j) {
                 const int* R = &buf[b][offs[b][j]];
                 const double* S = sm[b][j + 1];
-                const double* Sp = sm[b][j];
                 const int m = R[0];
                 double to = 0.0;
+                const double size = V / 2;
+                const double qc = size / S[2], qd = size / S[3];      // today's share counts
                 if (m > 0) {
                     const int nint = R[1], L = R[2];
-                    const double sizep = Vp / 2, size = V / 2;
                     for (int e = lane; e < m; e += 64) {              // term values |c - n|
                         const int sd = R[4 + e];
                         const int ps = sd / 3, ns = sd % 3;
-                        const double cv = ps == 0 ? sizep / Sp[2] : (ps == 1 ? -sizep / Sp[3] : 0.0);
-                        const double nv = ns == 0 ? size / S[2] : (ns == 1 ? -size / S[3] : 0.0);
+                        // (-x) / y == -(x / y) exactly: the reference's -size / sum
+                        const double cv = ps == 0 ? qa : (ps == 1 ? -qb : 0.0);
+                        const double nv = ns == 0 ? qc : (ns == 1 ? -qd : 0.0);
                         const double d = cv - nv;
                         node[e] = d < 0 ? -d : d;
                     }
@@ -943,7 +947,8 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                     turnover[i] = to;
                     value[i + 1] = Vn;
                 }
-                Vp = V;
+                qa = qc;
+                qb = qd;
                 V = Vn;
                 lds_sync();                                           // node[] reused next date
             }
