@@ -15,8 +15,8 @@ One ``step()`` over a device-resident calendar-grid panel:
 
 All buffers are allocated once and there is no host synchronisation inside a step.  Stages
 4-7 need only the Grams of the train+valid dates, and nothing downstream reads stage 3.  So the
-main stream runs 1 -> 2 (train+valid dates) -> 4 -> 7 while a side stream, forked after that
-Gram and joined at the end of the step, runs the test dates' Grams and stage 3.  The side work
+main stream runs 1 -> 2 (train+valid dates) -> 4 -> 7 while a side stream, forked after the
+pooled solve and joined at the end of the step, runs the test dates' Grams and stage 3.  The side work
 fills the GPU while the main chain runs its latency-bound tail (the PnL scan uses one CU).
 """
 from __future__ import annotations
@@ -108,6 +108,7 @@ class Pipeline:
         prio = os.environ.get("AFM_PIPE_PRIO", "1") != "0"
         self.main = torch.cuda.Stream(device=dev, priority=-8 if prio else 0)
         self.side = torch.cuda.Stream(device=dev, priority=0)
+        self.fork = os.environ.get("AFM_PIPE_FORK", "pooled")
 
     def step(self, events: dict | None = None, only=None):
         """One pass of the hot path.  ``events``: optional {stage: (start, end)} CUDA events.
@@ -150,23 +151,33 @@ class Pipeline:
                                       c.ycol, P(self.rows), 0, tt, P(self.gram), P(self.shift)),
                     "xs_gram")
                 mark("xs_gram", 1)
-            if on("xs_solve") or on("xs_gram_test"):
-                self.side.wait_stream(self.main)               # after the train+valid Grams
-                with torch.cuda.stream(self.side):
-                    hs = self.ctx.bind_stream()
-                    mark("xs_gram_test", 0)                    # test dates
-                    chk(L.afm_xs_gram_f64(hs, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p,
-                                          c.ycol, P(self.rows), tt, T - tt, P(self.gram[tt:]),
-                                          P(self.shift[tt:])), "xs_gram_test")
-                    mark("xs_gram_test", 1)
-                    if on("xs_solve"):
-                        mark("xs_solve", 0)
-                        chk(L.afm_ols_solve_f64(hs, P(self.gram), P(self.shift), p, T, c.tol,
-                                                P(self.beta), P(self.nobs), P(self.rank)),
-                            "ols_solve")
-                        chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1,
-                                                   P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
-                        mark("xs_solve", 1)
+
+            def side_chain():
+                if on("xs_solve") or on("xs_gram_test"):
+                    self.side.wait_stream(self.main)               # after the fork point
+                    with torch.cuda.stream(self.side):
+                        hs = self.ctx.bind_stream()
+                        mark("xs_gram_test", 0)                    # test dates
+                        chk(L.afm_xs_gram_f64(hs, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p,
+                                              c.ycol, P(self.rows), tt, T - tt, P(self.gram[tt:]),
+                                              P(self.shift[tt:])), "xs_gram_test")
+                        mark("xs_gram_test", 1)
+                        if on("xs_solve"):
+                            mark("xs_solve", 0)
+                            chk(L.afm_ols_solve_f64(hs, P(self.gram), P(self.shift), p, T, c.tol,
+                                                    P(self.beta), P(self.nobs), P(self.rank)),
+                                "ols_solve")
+                            chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1,
+                                                       P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
+                            mark("xs_solve", 1)
+
+            # fork the side stream after the pooled solve (AFM_PIPE_FORK=gram: right after the
+            # train+valid Grams): the pooled moments and the one-workgroup pooled solve then run
+            # without the side stream's Gram workgroups on their CUs (A/B on MI355X: 28.6-28.7
+            # vs 29.2-29.3 ms/step; forking after predict instead serialises the test Grams, 32 ms)
+            fork_late = self.fork == "pooled"
+            if not fork_late:
+                side_chain()
                 h = self.ctx.bind_stream()
             if on("pooled_ols"):
                 mark("pooled_ols", 0)
@@ -176,6 +187,9 @@ class Pipeline:
                                         P(self.pool_beta), P(self.pool_n), P(self.pool_rank)),
                     "pool_solve")
                 mark("pooled_ols", 1)
+            if fork_late:
+                side_chain()
+                h = self.ctx.bind_stream()
             if on("predict"):
                 mark("predict", 0)
                 chk(L.afm_predict_f64(h, P(self.out), T * lda, lda, self.t_test, T - self.t_test,
