@@ -124,10 +124,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a box with fewer GPUs than ranks: ranks share devices
+    # round-robin and AFM_BENCH_BACKEND=gloo replaces RCCL (the driver's N-GPU runs use neither)
+    ndev = torch.cuda.device_count()
+    if ndev:
+        local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("AFM_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     t0 = time.perf_counter()
     p = make_panel(args.assets, args.days, seed=args.seed)
