@@ -16,8 +16,8 @@ One ``step()`` over a device-resident calendar-grid panel:
 All buffers are allocated once and there is no host synchronisation inside a step.  Stages
 4-7 need only the Grams of the train+valid dates, and nothing downstream reads stage 3.  So the
 main stream runs 1 -> 2 (train+valid dates) -> 4 -> 7 while a side stream, forked after the
-pooled solve and joined at the end of the step, runs the test dates' Grams and stage 3.  The side work
-fills the GPU while the main chain runs its latency-bound tail (the PnL scan uses one CU).
+pooled solve and joined at the end of the step, runs the test dates' Grams and stage 3.  The side
+work fills the GPU while the main chain runs its latency-bound tail (the PnL scan uses one CU).
 """
 from __future__ import annotations
 
@@ -158,9 +158,10 @@ class Pipeline:
                     with torch.cuda.stream(self.side):
                         hs = self.ctx.bind_stream()
                         mark("xs_gram_test", 0)                    # test dates
-                        chk(L.afm_xs_gram_f64(hs, P(self.out), T * lda, lda, g.A, -1, P(self.cols), p,
-                                              c.ycol, P(self.rows), tt, T - tt, P(self.gram[tt:]),
-                                              P(self.shift[tt:])), "xs_gram_test")
+                        chk(L.afm_xs_gram_f64(hs, P(self.out), T * lda, lda, g.A, -1,
+                                              P(self.cols), p, c.ycol, P(self.rows), tt, T - tt,
+                                              P(self.gram[tt:]), P(self.shift[tt:])),
+                            "xs_gram_test")
                         mark("xs_gram_test", 1)
                         if on("xs_solve"):
                             mark("xs_solve", 0)
@@ -168,7 +169,8 @@ class Pipeline:
                                                     P(self.beta), P(self.nobs), P(self.rank)),
                                 "ols_solve")
                             chk(L.afm_fama_macbeth_f64(hs, P(self.beta), P(self.rank), T, p + 1,
-                                                       P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
+                                                       P(self.fm_mean), P(self.fm_t)),
+                                "fama_macbeth")
                             mark("xs_solve", 1)
 
             # fork the side stream after the pooled solve (AFM_PIPE_FORK=gram: right after the

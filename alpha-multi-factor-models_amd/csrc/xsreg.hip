@@ -1072,7 +1072,9 @@ static int pool_tree(afm_ctx* ctx, const double* gram, const double* shift, int 
     const int p2 = p + 2;
     const unsigned ny = pool_split(p2);
     // (a level over one segment is an exact identity merge: from n = 0 the Chan factor is 0)
-    auto blocks = [](int64_t n, int64_t per) -> int64_t { return n <= per ? 1 : (n + per - 1) / per; };
+    auto blocks = [](int64_t n, int64_t per) -> int64_t {
+        return n <= per ? 1 : (n + per - 1) / per;
+    };
     const int64_t nb0 = blocks(nseg, pool_level_per(level0));
     double* work = nullptr;
     if (nb0 > 1) {
