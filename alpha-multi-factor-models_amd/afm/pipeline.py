@@ -176,9 +176,8 @@ class Pipeline:
             # fork the side stream after the pooled solve (AFM_PIPE_FORK=gram: right after the
             # train+valid Grams): the pooled moments and the one-workgroup pooled solve then run
             # without the side stream's Gram workgroups on their CUs (A/B on MI355X: 28.6-28.7
-            # vs 29.2-29.3 ms/step; forking after predict instead serialises the test Grams, 32 ms)
-            fork_late = self.fork == "pooled"
-            if not fork_late:
+            # vs 29.2-29.3 ms/step; AFM_PIPE_FORK=predict, after the predictions: the same time)
+            if self.fork == "gram":
                 side_chain()
                 h = self.ctx.bind_stream()
             if on("pooled_ols"):
@@ -189,7 +188,7 @@ class Pipeline:
                                         P(self.pool_beta), P(self.pool_n), P(self.pool_rank)),
                     "pool_solve")
                 mark("pooled_ols", 1)
-            if fork_late:
+            if self.fork == "pooled":
                 side_chain()
                 h = self.ctx.bind_stream()
             if on("predict"):
@@ -198,6 +197,9 @@ class Pipeline:
                                       P(self.cols), p, P(self.pool_beta), 0, P(self.finite),
                                       c.ycol, P(self.pred)), "predict")
                 mark("predict", 1)
+            if self.fork == "predict":
+                side_chain()
+                h = self.ctx.bind_stream()
             if on("rebalance"):
                 mark("rebalance", 0)
                 r = self.reb
