@@ -26,7 +26,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from .factors import N_FACTORS, TARGET
+from .factors import N_FACTORS, TARGET, TMR
 from .grid import PanelGrid
 from .portfolio import MAX_BOOK
 
@@ -109,6 +109,7 @@ class Pipeline:
         self.main = torch.cuda.Stream(device=dev, priority=-8 if prio else 0)
         self.side = torch.cuda.Stream(device=dev, priority=0)
         self.fork = os.environ.get("AFM_PIPE_FORK", "pooled")
+        self.labels_at = os.environ.get("AFM_PIPE_LABELS", "after")
 
     def step(self, events: dict | None = None, only=None):
         """One pass of the hot path.  ``events``: optional {stage: (start, end)} CUDA events.
@@ -135,14 +136,27 @@ class Pipeline:
             h = self.ctx.bind_stream()
             if on("factors"):
                 mark("factors", 0)
-                # (label planes in the same call: on a side stream next to the latency-bound
-                # factor kernel they slowed it by more than their own time -- A/B on MI355X,
-                # 2500-asset shard 5.5 -> 7.1 ms -- and the Grams read the target plane)
-                chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), P(g.ret1d),
-                                      P(g.excess), P(g.vbits), P(self.out), P(self.nanfree),
-                                      P(self.finite)), "factors")
+                # label planes on the side stream, enqueued AFTER the factor kernel: its 236
+                # workgroups are dispatched first and the labels take the 20 CUs they leave free
+                # (A/B on MI355X: 28.50-28.62 vs 28.67-28.77 ms/step with the labels in the factor
+                # call, AFM_PIPE_LABELS=main).  Enqueued before it, they slowed the latency-bound
+                # factor kernel by more than their own time (2500-asset shard 5.5 -> 7.1 ms).
+                lab = self.labels_at == "main"
+                chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume),
+                                      P(g.ret1d) if lab else None, P(g.excess) if lab else None,
+                                      P(g.vbits), P(self.out), P(self.nanfree), P(self.finite)),
+                    "factors")
+                if not lab:
+                    with torch.cuda.stream(self.side):
+                        hs = self.ctx.bind_stream()
+                        chk(L.afm_labels_f64(hs, T, lda, 0, T, P(g.excess), P(g.ret1d),
+                                             P(g.vbits), P(self.out[TARGET]), P(self.out[TMR])),
+                            "labels")
+                    h = self.ctx.bind_stream()
                 chk(L.afm_drop_last_obs_bits(h, T, lda, P(g.vbits), P(self.finite), P(self.rows)),
                     "label rows")
+                if not lab:
+                    self.main.wait_stream(self.side)           # the Grams read the target plane
                 mark("factors", 1)
             tt = self.t_test
             if on("xs_gram"):                                  # train + valid dates
