@@ -58,6 +58,16 @@ SIGNATURES = {
     "afm_xs_series_f64": (I32, [P, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
     "afm_zscore_stats_f64": (I32, [P, P, I64, I64, I64, P, I32, P, I64, I64, P, P]),
     "afm_zscore_apply_f64": (I32, [P, P, I64, I64, I64, P, I32, P, I64, I64, P, P, P, I64, P, P]),
+    "afm_zgram_part_bytes": (I32, [I32]),
+    "afm_zstats_finalize_f64": (I32, [P, P, P, I32, I64, P, P]),
+    "afm_row_bits": (I32, [P, I64, I64, P, P, P, I64, I64, P]),
+    "afm_zgram_f64": (I32, [P, P, I64, I64, P, P, I32, I32, P, I32, P, I64, I64, I32, I64, I64,
+                            I64, P, I32]),
+    "afm_zpool_f64": (I32, [P, P, I64, I64, P, P, I32, I32, P, I32, P, I64, I64, I64, I32, I64,
+                            I32, P, I32]),
+    "afm_gram_tree_f64": (I32, [P, I32, P, I64, I32, I32, P]),
+    "afm_zpredict_f64": (I32, [P, P, I64, I64, I64, I64, P, I32, P, P, P, P]),
+    "afm_lasso_fit_f64": (I32, [P, P, P, I32, DBL, I32, DBL, I32, P, P]),
 }
 
 

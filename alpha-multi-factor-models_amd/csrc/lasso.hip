@@ -34,13 +34,19 @@ __device__ __forceinline__ double pick(double v0, double v1, int j) {
 }
 __device__ __forceinline__ double fsign(double f) { return f == 0.0 ? 0.0 : (f > 0.0 ? 1.0 : -1.0); }
 
+// alpha_row >= 0: alpha = alpha_row * n (sklearn's alpha times the row count, read on the device);
+// shift / beta_out (optional): beta_out = [intercept, w] with sklearn's _set_intercept,
+// intercept = y_offset - X_offset . w over the pooled means (shift + G'[0][.] / n).
 __global__ __launch_bounds__(64) void lasso_cd_kernel(const double* gram, int p, double alpha,
                                                       double beta, int max_iter, double tol,
-                                                      int positive, double* w_out, double* info) {
+                                                      int positive, double* w_out, double* info,
+                                                      double alpha_row, const double* shift,
+                                                      double* beta_out) {
     extern __shared__ double Q[];                    // [p][p] centered X'X
     const int lane = threadIdx.x;
     const int p2 = p + 2;
     const double n = gram[0];
+    if (alpha_row >= 0.0) alpha = alpha_row * n;
     // centered moments C = G'[1:,1:] - (g0 g0^T) / n of [x, y] (oracle.centered_moments)
     for (int e = lane; e < p * p; e += 64) {
         const int i = e / p, j = e - i * p;
@@ -112,8 +118,18 @@ __global__ __launch_bounds__(64) void lasso_cd_kernel(const double* gram, int p,
             if (gap < tol_y) break;
         }
     }
-    if (has0) w_out[j0] = w0;
-    if (has1) w_out[j1] = w1;
+    if (w_out) {
+        if (has0) w_out[j0] = w0;
+        if (has1) w_out[j1] = w1;
+    }
+    if (beta_out) {
+        if (has0) beta_out[1 + j0] = w0;
+        if (has1) beta_out[1 + j1] = w1;
+        double xw = 0.0;                             // X_offset . w, feature order
+        for (int j = 0; j < p; ++j)
+            xw = xw + (shift[1 + j] + gram[1 + j] / n) * pick(w0, w1, j);
+        if (lane == 0) beta_out[0] = (shift[1 + p] + gram[1 + p] / n) - xw;
+    }
     if (lane == 0) {
         info[0] = gap;
         info[1] = tol_y;
@@ -141,7 +157,26 @@ extern "C" int afm_lasso_cd_f64(afm_ctx* ctx, const double* gram, int p, double 
         attr = true;
     }
     hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(64), lds, ctx->stream, gram, p,
-                       alpha_n, beta, max_iter, tol, positive, w, info);
+                       alpha_n, beta, max_iter, tol, positive, w, info, -1.0,
+                       (const double*)nullptr, (double*)nullptr);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_lasso_fit_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
+                                 double alpha, int max_iter, double tol, int positive,
+                                 double* beta_out, double* info) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(p >= 1 && p <= afm::kMaxLassoP, "need 1 <= p <= 110");
+    AFM_CHECK_ARG(gram && shift && beta_out && info, "null buffer");
+    AFM_CHECK_ARG(max_iter >= 1 && alpha >= 0 && tol >= 0, "bad max_iter / alpha / tol");
+    const int lds = (int)sizeof(double) * p * p;
+    AFM_HIP(hipFuncSetAttribute((const void*)afm::lasso_cd_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
+    hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(64), lds, ctx->stream, gram, p, 0.0,
+                       0.0, max_iter, tol, positive, (double*)nullptr, info, alpha, shift,
+                       beta_out);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

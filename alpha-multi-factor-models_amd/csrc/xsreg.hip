@@ -678,10 +678,12 @@ __global__ __launch_bounds__(512, 1) void gram_kernel(GramArgs g) {
 // (row i at i(i+1)/2: 38 KB at p = 96, so four workgroups share a CU where the square layout's
 // 76 KB allowed two; every access is on or below the diagonal).
 struct SolveArgs {
-    const double* gram;      // [nseg][p2][p2]
-    const double* shift;     // [nseg][p2]
+    const double* gram;      // [nseg][pg + 2][pg + 2]
+    const double* shift;     // [nseg][pg + 2]
     int p;
     double tol;
+    const int32_t* sel;      // optional [p]: regressor i is Gram feature sel[i] (0-based); y = pg
+    int pg;                  // features of the Gram (p when sel is null)
     double* beta;            // [nseg][p+1]: intercept, beta_1..p
     double* nobs;            // [nseg]
     int32_t* rank;           // [nseg]
@@ -696,11 +698,16 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
     __shared__ double mean[kMaxP + 2];
     __shared__ double bvec[kMaxP];
     __shared__ int drop[kMaxP];
+    __shared__ int gx[kMaxP + 2];                    // Gram index of augmented column r (0: ones)
     const int tid = threadIdx.x;
-    const int p = s.p, p2 = p + 2, q = p + 1;
+    const int p = s.p, q = p + 1;
+    const int p2 = s.pg + 2;                         // Gram dimension
     auto row = [](int i) { return i * (i + 1) / 2; };      // offset of row i
     const double* G = s.gram + (int64_t)blockIdx.x * p2 * p2;
     const double* sf = s.shift + (int64_t)blockIdx.x * p2;
+    for (int r = tid; r <= q; r += kThreads)
+        gx[r] = r == 0 ? 0 : (r == q ? s.pg + 1 : (s.sel ? 1 + s.sel[r - 1] : r));
+    __syncthreads();
     const double n = G[0];
     double* beta = s.beta + (int64_t)blockIdx.x * (p + 1);
     if (tid == 0) s.nobs[blockIdx.x] = n;
@@ -709,9 +716,10 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
         if (tid == 0) s.rank[blockIdx.x] = 0;
         return;
     }
-    for (int j = tid; j < p2; j += kThreads) mean[j] = (j == 0) ? 1.0 : G[j] / n;   // shifted
+    for (int j = tid; j <= q; j += kThreads) mean[j] = (j == 0) ? 1.0 : G[gx[j]] / n;   // shifted
     for (int r = tid; r < q; r += kThreads) {
-        const double d = G[(r + 1) * p2 + r + 1] - G[r + 1] * G[r + 1] / n;
+        const int gr = gx[r + 1];
+        const double d = G[gr * p2 + gr] - G[gr] * G[gr] / n;
         dsc[r] = r < p ? (d > 0 ? 1.0 / __builtin_sqrt(d) : 0.0) : 1.0;
         if (r < p) drop[r] = !(d > 0);
     }
@@ -719,7 +727,8 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
     // lower triangle of D C D (packed rows)
     for (int r = tid >> 4; r < q; r += kThreads >> 4)
         for (int c = tid & 15; c <= r; c += 16) {
-            const double v = G[(r + 1) * p2 + c + 1] - G[r + 1] * G[c + 1] / n;
+            const int gr = gx[r + 1], gc = gx[c + 1];
+            const double v = G[gr * p2 + gc] - G[gr] * G[gc] / n;
             M[row(r) + c] = v * dsc[r] * dsc[c];
         }
     __syncthreads();
@@ -757,7 +766,7 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
         for (int j = lane; j < p; j += 64) {
             const double b = bvec[j] * dsc[j];
             beta[1 + j] = b;
-            part = part + (sf[1 + j] + mean[1 + j]) * b;
+            part = part + (sf[gx[1 + j]] + mean[1 + j]) * b;
             rk += drop[j] ? 0 : 1;
         }
         for (int o = 32; o > 0; o >>= 1) {
@@ -765,7 +774,7 @@ __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
             rk += __shfl_xor(rk, o, 64);
         }
         if (lane == 0) {
-            beta[0] = (sf[p + 1] + mean[p + 1]) - part;
+            beta[0] = (sf[gx[q]] + mean[q]) - part;
             s.rank[blockIdx.x] = rk;
         }
     }
@@ -1049,7 +1058,7 @@ extern "C" int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double*
     AFM_CHECK_ARG(p >= 1 && p <= kMaxP, "need 1 <= p <= 110");
     AFM_CHECK_ARG(gram && shift && beta && nobs && rank, "null buffer");
     if (nseg <= 0) return AFM_OK;
-    SolveArgs s{gram, shift, p, tol, beta, nobs, rank};
+    SolveArgs s{gram, shift, p, tol, nullptr, p, beta, nobs, rank};
     const size_t lds = sizeof(double) * (size_t)(p + 1) * (p + 2) / 2;     // packed triangle
     AFM_HIP(hipFuncSetAttribute((const void*)ols_solve_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

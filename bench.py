@@ -3,12 +3,15 @@
 (BASELINE.json ``metric``), SURVEY.md §8(d).
 
 Workload (N=1): BASELINE.json configs[2] -- 10,000 assets x 20 years (5,040 trading days) daily
-synthetic panel (seeded generator, SURVEY.md §8(d): ragged listings, 0.2% holes), inputs
-resident in HBM before the timed region.  One step = afm.pipeline.Pipeline.step(): 98-column
-factor build, per-date OLS of next-day excess return on all 96 factors (fp64 MFMA Grams) + FM
-stats, pooled OLS over the train+valid dates, predictions on the test dates (last 20%),
-rolling-252-day covariance + exact min-variance KKT weights for top/bottom-10 books on every
-test date, PnL/turnover scan.
+synthetic panel (seeded generator, SURVEY.md §8(d): ragged listings, 0.2% holes, 90% tradable),
+inputs resident in HBM before the timed region.  One step = afm.pipeline.Pipeline.step(), the
+reference chain that feeds PortfolioManager: 98-column factor build (NT:1-93) -> train-window
+per-security z-score of the 97 features (KKT:424-458, the reference's split dates) -> per-date
+Grams of [1, z_1..z_97, target] on fp64 MFMA -> pooled train+valid moments + Lasso(alpha=2e-4)
+(KKT:605-607) -> test predictions (KKT:612) -> rolling-252-day covariance + exact min-variance
+KKT weights for top/bottom-10 books on every test date + PnL/turnover scan (KKT:976-977); side
+streams: AlphaSignalAnalyzer on the predictions (KKT:630-631) and the per-date FM30 OLS +
+Fama-MacBeth (north-star extension).
 
 Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 is launched by torch.distributed.run
 (one rank per GPU).  Rank 0 prints ONE JSON line.
@@ -38,7 +41,7 @@ def log(*a):
 # FETCH_SIZE x2 and KiB corrections of MI355X_MICROARCH.md applied there)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 ROOF_KERNELS = {"factors": ("factor_panel_kernel", "masks_kernel", "labels_kernel"),
-                "xs_gram": ("gram_kernel",)}
+                "xs_gram": ("zgram_kernel",)}
 
 
 def pmc_traffic(stage: str, assets: int, days: int):
@@ -57,49 +60,26 @@ def pmc_traffic(stage: str, assets: int, days: int):
     return sum(ks[k]["hbm_bytes"] for k in ROOF_KERNELS[stage])
 
 
-def cpu_baseline(seed: int, assets: int = 500, days: int = 2520):
-    """The oracle chain (C factor restatement + numpy per-date lstsq + sklearn pooled OLS +
-    numpy/Python portfolio with the exact QP), 1 core, on config A (500 assets x 2520 days)."""
+def cpu_baseline(seed: int, assets: int = 150, days: int = 2520):
+    """The oracle chain (oracle/chain.py: C factor restatement, numpy z-score, scikit-learn Lasso,
+    exact-QP PortfolioManager, analyzer, per-date FM lstsq), 1 core, on a bounded sample of
+    config A's calendar (``assets`` x 2,520 days; the reference's own split rule)."""
     import numpy as np
     from threadpoolctl import threadpool_limits
 
-    import oracle
-    from oracle import pipeline as PL
-    from oracle import portfolio as PF
+    from afm.pipeline import FM30
     from afm.synthetic import make_panel
-    p = make_panel(assets, days, seed=seed)
-    v = p.valid[:, :p.A]
-    aa, tt = np.nonzero(v.T)
-    off = np.r_[0, np.cumsum(v.sum(axis=0))].astype(np.int64)
-    cols = [np.ascontiguousarray(x[tt, aa]) for x in (p.close, p.volume, p.ret1d, p.excess)]
-    n_ad = len(tt)
-    limiter = threadpool_limits(1)                                       # 1 core, BLAS included
-    t0 = time.perf_counter()
-    fac = oracle.factors_long(off, *cols)                               # factors
-    t1 = time.perf_counter()
-    X, y = fac[:, :96], fac[:, 96]
-    use = np.isfinite(X).all(axis=1) & np.isfinite(y)
-    T = days
-    t_test = int(T * 0.8)
-    PL.xs_ols(tt[use], X[use], y[use])                                   # per-date OLS
-    t2 = time.perf_counter()
-    tv = use & (tt < t_test)
-    b0, b = PL.pooled_ols(X[tv], y[tv])                                  # pooled OLS
-    te = use & (tt >= t_test) & (tt < T - 1)
-    pred = b0 + X[te] @ b
-    t3 = time.perf_counter()
-    ids = p.ids[aa]
-    dates = p.dates[tt].astype(np.int64)
-    trad = p.tradable[tt, aa]
-    PF.run_portfolio(dates[te], ids[te], pred, dates, ids, y, dates, ids, trad,   # KKT stage
-                     cols[0], fac[:, 97], window=252)
-    t4 = time.perf_counter()
-    limiter.unregister() if hasattr(limiter, "unregister") else None
-    total = t4 - t0
+    from oracle import chain
+    p = make_panel(assets, days, seed=seed, tradable_p=0.9)
+    n_ad = int(p.valid.sum())
+    tm = {}
+    with threadpool_limits(1):                                       # 1 core, BLAS included
+        t0 = time.perf_counter()
+        chain.run_chain(p, "2006-12-29", "2007-12-31", fm_features=FM30, timings=tm)
+        total = time.perf_counter() - t0
     return {"value": round(n_ad / total, 1), "unit": "asset-days/s", "cores": 1, "kind": "port",
-            "sample": f"oracle chain on config A ({assets} assets x {days} days = {n_ad} "
-                      f"asset-days): factors {t1 - t0:.2f}s, per-date OLS {t2 - t1:.2f}s, pooled "
-                      f"OLS+predict {t3 - t2:.2f}s, rebalance+KKT+PnL {t4 - t3:.2f}s"}
+            "sample": f"oracle chain (oracle/chain.py) on {assets} assets x {days} days = {n_ad} "
+                      f"asset-days: " + ", ".join(f"{k} {v:.2f}s" for k, v in tm.items())}
 
 
 def main():
@@ -110,6 +90,7 @@ def main():
     ap.add_argument("--assets", type=int, default=10000)
     ap.add_argument("--days", type=int, default=5040)
     ap.add_argument("--seed", type=int, default=2023)
+    ap.add_argument("--top-n", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -118,48 +99,51 @@ def main():
     import torch.distributed as dist
 
     import afm
-    from afm.pipeline import PIPELINE_STAGES, Pipeline
+    from afm.pipeline import PIPELINE_STAGES, Pipeline, PipelineConfig
     from afm.synthetic import make_panel
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal of the multi-rank path on a box with fewer GPUs than ranks: ranks share devices
-    # round-robin and AFM_BENCH_BACKEND=gloo replaces RCCL (the driver's N-GPU runs use neither)
+    backend = os.environ.get("AFM_BENCH_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
-    if ndev:
-        local = local % ndev
+    if backend == "gloo" and ndev:
+        local = local % ndev          # rehearsal only: gloo ranks may share a GPU
+    elif ndev and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} visible GPUs")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("AFM_BENCH_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     t0 = time.perf_counter()
-    p = make_panel(args.assets, args.days, seed=args.seed)
+    p = make_panel(args.assets, args.days, seed=args.seed, tradable_p=0.9)
     grid = afm.PanelGrid.from_panel(p, device=dev)
     del p
     n_ad = grid.n_asset_days()                         # the whole panel (strong scaling)
+    cfg = PipelineConfig(top_n=args.top_n)
     if world > 1:
         from afm.sharded import EXCHANGE_STAGES, Comm, ShardedPipeline
-        pipe = ShardedPipeline(grid, Comm())
+        pipe = ShardedPipeline(grid, Comm(), cfg)
         stages = EXCHANGE_STAGES
         n_ad_local = pipe.n_asset_days_local()
     else:
-        pipe = Pipeline(grid)
+        pipe = Pipeline(grid, cfg)
         stages = PIPELINE_STAGES
         n_ad_local = n_ad
     torch.cuda.synchronize()
     log(f"[rank {rank}] panel {grid.A}x{grid.T} ({n_ad} asset-days, {n_ad_local} in this rank's "
-        f"factor shard) ready in {time.perf_counter() - t0:.1f}s")
+        f"factor shard) ready in {time.perf_counter() - t0:.1f}s; split {pipe.sp}")
 
     for _ in range(args.warmup):
         pipe.step()
     torch.cuda.synchronize()
     if rank == 0 and args.warmup:
         s = pipe.summary()
-        log(f"[rank 0] warmup: final value {s['final_value']:.6g}, sharpe {s['sharpe']:.4g}, "
-            f"per-date ranks {np.bincount(s['ranks'])[-3:]}, qp status {np.bincount(s['status'])}")
+        log(f"[rank 0] warmup: final value {s['final_value']:.9g}, sharpe {s['sharpe']:.6g}, "
+            f"lasso n_iter {s['lasso_n_iter']} nnz {s['lasso_nnz']}, FM rank counts "
+            f"{np.bincount(s['fm_rank'])[-2:]}, k {np.bincount(s['k'])[-2:]}, qp status "
+            f"{np.bincount(s['status'])}, mean IC {s.get('ic_mean')}")
 
     evs = [{st: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for st in stages} for _ in range(args.steps)]
@@ -184,31 +168,36 @@ def main():
 
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        # roofline of the dominant kernel: factor panel (HBM) or the per-date Gram (fp64 MFMA)
-        p = pipe.p
+        p2 = pipe.p2
+        # roofline of the two dominant kernels, ranked by per-step device time: the factor panel
+        # (HBM: 816 B per asset-day) and the pooled Gram (fp64 MFMA:
+        # rows * (p+2)(p+3) flops over the train + valid rows, zpool + tree merges).
         fac_gbs = FACTOR_BYTES_PER_AD * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
-        if world == 1:      # stage xs_gram = the train+valid dates (the test dates: side stream)
-            gram_rows = float(pipe.nobs[:pipe.t_test].sum().item())
-        else:
-            gram_rows = float(pipe.nobs.sum().item()) / world  # this rank's share of the rows
-        gram_tfs = gram_rows * (p + 2) * (p + 3) / (stage_ms["xs_gram"] * 1e-3) / 1e12
+        rows_tv = float(pipe.pool_g[0, 0, 0].item())           # pooled rows (n of the Gram)
+        if pipe.sp.dup:
+            rows_tv -= float(pipe.te_gram[0, 0, 0].item())       # the duplicate is not recomputed
+        rows_tv /= (world if world > 1 else 1)
+        gram_tfs = rows_tv * p2 * (p2 + 1) / (stage_ms["xs_gram"] * 1e-3) / 1e12
         single = world == 1
-        if stage_ms["factors"] >= stage_ms["xs_gram"]:
-            tb = pmc_traffic("factors", args.assets, args.days) if single else None
-            roof = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(fac_gbs / HBM_PEAK_GBS, 4),
-                    "traffic": None if tb is None else round(tb / 1e9, 3),
-                    "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                    "algorithmic": round(FACTOR_BYTES_PER_AD * n_ad_local / 1e9, 3),
-                    "kernel": "+".join(ROOF_KERNELS["factors"]),
-                    "kernel_ms": round(stage_ms["factors"], 3)}
-        else:
-            tb = pmc_traffic("xs_gram", args.assets, args.days) if single else None
-            roof = {"bound": "mfma", "achieved": round(gram_tfs, 2), "peak": F64_MFMA_PEAK_TFS,
-                    "unit": "TFLOP/s", "frac": round(gram_tfs / F64_MFMA_PEAK_TFS, 4),
-                    "traffic": None if tb is None else round(tb / 1e9, 3),
-                    "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                    "kernel": "gram_kernel", "kernel_ms": round(stage_ms["xs_gram"], 3)}
+        fac = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(fac_gbs / HBM_PEAK_GBS, 4),
+               "traffic": None, "kernel": "factor_panel_kernel (+ row-bit kernels)",
+               "kernel_ms": round(stage_ms["factors"], 3),
+               "algorithmic_GB": round(FACTOR_BYTES_PER_AD * n_ad_local / 1e9, 3)}
+        tb = pmc_traffic("factors", args.assets, args.days) if single else None
+        if tb is not None:
+            fac["traffic"] = round(tb / 1e9, 3)
+            fac["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+        gram = {"bound": "mfma", "achieved": round(gram_tfs, 2), "peak": F64_MFMA_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": round(gram_tfs / F64_MFMA_PEAK_TFS, 4),
+                "traffic": None, "kernel": "zgram_kernel<7,1> + tree_merge_kernel (pooled train+valid Gram)",
+                "kernel_ms": round(stage_ms["xs_gram"], 3),
+                "algorithmic_GFLOP": round(rows_tv * p2 * (p2 + 1) / 1e9, 3)}
+        tg = pmc_traffic("xs_gram", args.assets, args.days) if single else None
+        if tg is not None:
+            gram["traffic"] = round(tg / 1e9, 3)
+        ranked = sorted([(stage_ms["factors"], fac), (stage_ms["xs_gram"], gram)],
+                        key=lambda x: -x[0])
         res = {
             "metric": "asset-days/sec, factor build+XS regression+KKT (10k assets x 20y), "
                       "1/2/4/8 GPU",
@@ -219,16 +208,18 @@ def main():
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "f64", "data": "synthetic (seeded OHLCV panel, SURVEY.md §8(d))",
             "config": {"workload": f"{args.assets} assets x {args.days} days daily panel: 98 "
-                                   f"factors -> per-date OLS on 96 factors + FM -> pooled OLS -> "
-                                   f"predict -> rolling-252 cov + exact KKT top/bottom-10 -> PnL",
+                                   f"factors -> train-window z-score (97 features) -> per-date "
+                                   f"MFMA Grams -> pooled Lasso -> predict -> rolling-252 cov + "
+                                   f"exact KKT top/bottom-{args.top_n} -> PnL; side: analyzer "
+                                   f"(IC/layers/top-10) + per-date FM30 OLS",
                        "assets": args.assets, "days": args.days, "asset_days": total_ad,
-                       "parallelism": (f"asset shards (factors, partial Grams) + date shards "
+                       "split": {"train_end": cfg.train_end, "valid_end": cfg.valid_end},
+                       "parallelism": (f"asset shards (factors, block Grams) + date shards "
                                        f"(solves, rebalance) x{world}") if world > 1
                        else "single"},
             "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
-            "roofline": roof,
-            "secondary": {"factor_panel_GBps": round(fac_gbs, 1),
-                          "gram_TFLOPs": round(gram_tfs, 2)},
+            "roofline": ranked[0][1],
+            "roofline_next": ranked[1][1],
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.seed)

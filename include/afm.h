@@ -249,6 +249,59 @@ int afm_zscore_apply_f64(afm_ctx* ctx, const double* base, int64_t col_stride, i
                          int64_t t0, int64_t t1, const double* mu, const double* sd, double* out,
                          int64_t out_col_stride, const int32_t* out_cols, uint64_t* keep);
 
+/* ---- the reference chain's regression on z-scored features (csrc/zgram.hip) ---------------
+ * Replaces the z-scored design matrices of KKT:446-458 (never materialised: z is computed where
+ * it is read) and the train+valid fit / test predict of KKT:582-612.
+ * afm_zstats_finalize_f64: mu, sd [K][lda] (afm_zscore_stats_f64) -> zs [K+1][lda][2] =
+ * {mu, 1/sd} (0, 0 where the column is unusable; row K = {0, 1}: identity for the regressand),
+ * asset_ok[lda] = every column has a finite mean and sd > 0 (the assets that survive the z-score
+ * dropna of KKT:452-454; every other asset has a NaN / inf z in all its rows). */
+int afm_zstats_finalize_f64(afm_ctx* ctx, const double* mu, const double* sd, int K, int64_t lda,
+                            double* zs, int32_t* asset_ok);
+/* out[c][a] = a[c][a] & b[c][a] (b optional) & (asset_ok[a] ? ~0 : 0) (optional), restricted to
+ * the dates [t0, t1): the split / dropna row sets on the calendar grid (KKT:426-458). */
+int afm_row_bits(afm_ctx* ctx, int64_t nch, int64_t lda, const uint64_t* a, const uint64_t* b,
+                 const int32_t* asset_ok, int64_t t0, int64_t t1, uint64_t* out);
+/* Bytes of one partial Gram of afm_zgram_f64 / afm_zpool_f64 for p regressors (accumulator
+ * layout: the upper-triangle 16 x 16 tile pairs of 2 tiles when p + 2 <= 32, else 7). */
+int afm_zgram_part_bytes(int p);
+/* Partial Grams of Z = [1, z_1..z_p, y] on fp64 MFMA (v_mfma_f64_16x16x4_f64), z_j = (x_j - mu)
+ * * (1/sd) with {mu, 1/sd} = zs row zcols[j] (DEVICE int32; NULL = row j), y = plane ycol scaled
+ * by zs row zid (the identity row of afm_zstats_finalize_f64); rows = set bits of `bits`;
+ * regressor j is plane cols[j].  1 <= p <= 106; grid = workgroups (0: one per CU).
+ * afm_zgram_f64 -- one partial per (date, asset block): dates [t0, t0+nt), block b = assets
+ *   [blk0 + b*blk_assets, + blk_assets) below a_end; part [nt][nblk][part].  The per-date Grams
+ *   of a regression on the cross-section (Fama-MacBeth).
+ * afm_zpool_f64 -- one partial per (row-block r, date chunk c): the 64 assets [blk0 + 64r, +64)
+ *   at every date of chunk c of [t0, t0+nt) (nchunk equal chunks); part [nrb][nchunk][part].
+ *   The pooled Gram of every (date, asset) row (the design matrix of KKT:583 / 606): a
+ *   workgroup keeps one row-block's {mu, 1/sd} in registers across its dates. */
+int afm_zgram_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
+                  const int32_t* cols, const int32_t* zcols, int p, int ycol, const double* zs,
+                  int zid, const uint64_t* bits, int64_t t0, int64_t nt, int nblk, int64_t blk0,
+                  int64_t blk_assets, int64_t a_end, double* part, int grid);
+int afm_zpool_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
+                  const int32_t* cols, const int32_t* zcols, int p, int ycol, const double* zs,
+                  int zid, const uint64_t* bits, int64_t t0, int64_t nt, int64_t blk0, int nrb,
+                  int64_t a_end, int nchunk, double* part, int grid);
+/* Fixed-tree sum of partials: group g adds the leaves [g*per, min((g+1)*per, total)) (per <= 32)
+ * over the binary tree of strides 1, 2, 4, 8, 16.  The tree composes -- a rank holding an aligned
+ * power-of-two run of leaves computes one of its subtrees -- so every GPU count gets bit-identical
+ * sums.  final_out: write symmetric Grams out[ngroups][p+2][p+2] (raw moments: entry [0][0] = n,
+ * row 0 = column sums), else merged partials out[ngroups][part]. */
+int afm_gram_tree_f64(afm_ctx* ctx, int p, const double* in, int64_t total, int per,
+                      int final_out, double* out);
+/* pred[t][a] = beta[0] + sum_j beta[1+j] * z_j (zero coefficients skipped), grid rows with a bit
+ * set, t in [t0, t0+nt); NaN on the other cells of those dates.  (Lasso.predict, KKT:612.) */
+int afm_zpredict_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
+                     int64_t t0, int64_t nt, const int32_t* cols, int p, const double* zs,
+                     const double* beta, const uint64_t* bits, double* pred);
+/* Lasso(alpha, max_iter, tol).fit on one pooled (gram, shift) of [1, x, y] -- afm_lasso_cd_f64
+ * with alpha_n = alpha * n read on the device, and beta_out[p+1] = [intercept, w] (sklearn's
+ * _set_intercept: mean(y) - mean(x) . w).  info[3] = {gap, tol * y'y, n_iter}. */
+int afm_lasso_fit_f64(afm_ctx* ctx, const double* gram, const double* shift, int p, double alpha,
+                      int max_iter, double tol, int positive, double* beta_out, double* info);
+
 #ifdef __cplusplus
 }
 #endif
