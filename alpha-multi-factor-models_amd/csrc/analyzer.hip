@@ -11,13 +11,16 @@
 //  xs_rank_kernel       A3/A4 per date: exact ranks (method='first': ties by row position),
 //                           ascending and descending, from 2048-row LDS bitonic-sorted chunks +
 //                           binary-search merge counts.
-//  xs_stats_kernel      A2-A4 one lane per (date, return type): pandas nancorr Welford IC
-//                           (return = the later column), Kahan group means per decile layer
-//                           (layer = int(rank/n*10)+1, KKT:328-330), factor-weighted top-10
-//                           returns summed in the string-sorted pivot column order (KKT:362-369).
+//  xs_stats_kernel      A2-A4 one workgroup per date, rows staged through LDS; in lanes: pandas
+//                           nancorr Welford IC (return = the later column), Kahan group means per
+//                           decile layer (layer = int(rank/n*10)+1, KKT:328-330), factor-weighted
+//                           top-10 returns summed in the string-sorted pivot column order
+//                           (KKT:362-369).
 //  xs_series_kernel     A2-A4 cumulative layer / long-short / top-k series and the per-year IR
 //                           (pairwise mean / two-pass std of the IC values, KKT:353).
 #include "afm_internal.h"
+
+#include <algorithm>
 
 #pragma clang fp contract(off)
 
@@ -80,19 +83,23 @@ __global__ __launch_bounds__(256) void fwd_returns_kernel(int64_t T, int64_t lda
 }
 
 // ---- block helpers ---------------------------------------------------------------------------
+// exclusive scan of 0/1 flags over the 256 threads: ballots within the waves, wave totals
+// through LDS (two barriers instead of a log-step scan)
 __device__ int block_scan(int v, int* sbuf, int* excl) {
-    const int tid = threadIdx.x;
-    sbuf[tid] = v;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const u64 m = __ballot(v != 0);
+    const int below = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    if (lane == 0) sbuf[w] = __popcll(m);
     __syncthreads();
-    for (int off = 1; off < kT; off <<= 1) {
-        int x = tid >= off ? sbuf[tid - off] : 0;
-        __syncthreads();
-        sbuf[tid] += x;
-        __syncthreads();
+    int off = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kT / 64; ++i) {
+        off += i < w ? sbuf[i] : 0;
+        total += sbuf[i];
     }
-    *excl = sbuf[tid] - v;
-    int total = sbuf[kT - 1];
     __syncthreads();
+    *excl = off + below;
     return total;
 }
 
@@ -240,9 +247,11 @@ struct RankArgs {
     int32_t* rank_desc;       // [T][lda]
 };
 
-__global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g) {
-    __shared__ u64 key[kChunk];
-    __shared__ int32_t idx[kChunk];
+__global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g, int lds_rows) {
+    // dynamic LDS: phase 1 the sort buffers, phase 2 (n <= lds_rows) the date's sorted chunks
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    u64* key = reinterpret_cast<u64*>(dyn);
+    int32_t* idx = reinterpret_cast<int32_t*>(dyn + sizeof(u64) * kChunk);
     const int tid = threadIdx.x;
     const int64_t t = blockIdx.x;
     const int n = g.nrows[t];
@@ -284,14 +293,25 @@ __global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g) {
         }
         __syncthreads();
     }
-    // rank of every row = sum over chunks of its lower-bound position (keys then row position)
+    // rank of every row = sum over chunks of its lower-bound position (keys then row position);
+    // the searches read the sorted chunks from LDS when the whole date fits
+    const bool in_lds = n <= lds_rows;
+    u64* LK = reinterpret_cast<u64*>(dyn);
+    int32_t* LI = reinterpret_cast<int32_t*>(dyn + sizeof(u64) * (size_t)lds_rows);
+    if (in_lds && nch > 1) {
+        for (int e = tid; e < n; e += kT) {
+            LK[e] = g.skey[base + e];
+            LI[e] = g.sidx[base + e];
+        }
+        __syncthreads();
+    }
     for (int e = tid; e < n; e += kT) {
         const u64 k0 = okey(g.rows[base + e]);
         int less = 0, greater = 0;
         for (int c = 0; c < nch; ++c) {
             const int c0 = c * kChunk, len = min(kChunk, n - c0);
-            const u64* K = g.skey + base + c0;
-            const int32_t* I = g.sidx + base + c0;
+            const u64* K = in_lds ? (nch > 1 ? LK + c0 : key) : g.skey + base + c0;
+            const int32_t* I = in_lds ? (nch > 1 ? LI + c0 : idx) : g.sidx + base + c0;
             // lb: first position with (key, idx) >= (k0, e)
             int lo = 0, hi = len;
             while (lo < hi) {
@@ -330,88 +350,119 @@ struct StatArgs {
     double* port;             // [nd][3]
 };
 
-__global__ __launch_bounds__(64) void xs_stats_kernel(StatArgs g) {
-    const int64_t gid = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (gid >= g.nd * 3) return;
-    const int64_t di = gid / 3;
-    const int k = (int)(gid % 3);
+// One workgroup (2 waves) per date.  Rows are staged through LDS in chunks (all 128 threads:
+// the 4 value columns, each row's decile layer from its rank, the top-10 pivot cells); then the
+// sequential recurrences run in lanes, each over the rows in order -- the operations of the
+// reference, only spread over lanes:
+//   wave 0, lanes 0..2    nancorr Welford of (return_k, factor) (KKT:344-345)
+//   wave 1, lanes 0..29   Kahan group mean of return_k over the rows of layer l (k = lane / 10,
+//                         l = lane % 10; groupby(['date', 'layer']).mean(), KKT:331-332)
+// and lanes 0..2 of wave 0 finish the factor-weighted top-10 sums (KKT:362-369).
+constexpr int kStatRows = 512;
+
+__global__ __launch_bounds__(128) void xs_stats_kernel(StatArgs g) {
+    __shared__ double sv[4][kStatRows];          // factor, return_1, return_2, return_5
+    __shared__ int8_t slay[kStatRows];
+    __shared__ double pv_f[kTopK], pv_r[3][kTopK];
+    __shared__ int pv_has[kTopK];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t di = blockIdx.x;
     const int64_t t = g.dates[di];
     const int n = g.nrows[t];
     const int64_t plane = g.T * g.lda;
     const int64_t base = t * g.lda;
-    const double* F = g.rows + base;
-    const double* Rk = g.rows + (1 + k) * plane + base;
-    // nancorr(return_k, factor): vx = return (later column), vy = factor
+    if (tid < kTopK) { pv_has[tid] = 0; pv_f[tid] = qnan(); }
+    if (tid < 3 * kTopK) pv_r[tid / kTopK][tid % kTopK] = qnan();
+    // wave 0 lanes 0..2: Welford state; wave 1 lanes 0..29: Kahan state
+    const int k0 = lane;                                   // wave 0: return type
+    const int k1 = lane / kLayers, l1 = lane % kLayers;    // wave 1: (type, layer)
     double nobs = 0, mx = 0, my = 0, sxx = 0, syy = 0, sxy = 0;
-    double lsum[kLayers], lcomp[kLayers];
-    int lcnt[kLayers];
-    for (int l = 0; l < kLayers; ++l) { lsum[l] = 0; lcomp[l] = 0; lcnt[l] = 0; }
-    double pv_f[kTopK], pv_r[kTopK];
-    bool pv_has[kTopK];
-    for (int j = 0; j < kTopK; ++j) { pv_f[j] = qnan(); pv_r[j] = qnan(); pv_has[j] = false; }
-    for (int e = 0; e < n; ++e) {
-        const double vy = F[e], vx = Rk[e];
-        if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
-            nobs += 1;
-            const double dx = vx - mx, dy = vy - my;
-            mx += 1. / nobs * dx;
-            my += 1. / nobs * dy;
-            sxx += (vx - mx) * dx;
-            syy += (vy - my) * dy;
-            sxy += (vx - mx) * dy;
+    double lsum = 0, lcomp = 0;
+    int lcnt = 0;
+    for (int c0 = 0; c0 < n; c0 += kStatRows) {
+        const int len = min(kStatRows, n - c0);
+        __syncthreads();                                   // the previous chunk is consumed
+        for (int e = tid; e < len; e += 128) {
+            const int64_t o = base + c0 + e;
+            sv[0][e] = g.rows[o];
+            for (int q = 0; q < 3; ++q) sv[1 + q][e] = g.rows[(1 + q) * plane + o];
+            const double pct = (double)g.rank_asc[o] / (double)n;     // KKT:328-330
+            int layer = (int)(pct * kLayers) + 1;
+            if (layer > kLayers) layer = kLayers;
+            slay[e] = (int8_t)(layer - 1);
+            const int rd = g.rank_desc[o];
+            if (rd <= kTopK) {
+                pv_f[rd - 1] = sv[0][e];
+                for (int q = 0; q < 3; ++q) pv_r[q][rd - 1] = sv[1 + q][e];
+                pv_has[rd - 1] = 1;
+            }
         }
-        // layer (KKT:328-330) and Kahan group mean (groupby(['date','layer']).mean())
-        const double pct = (double)g.rank_asc[base + e] / (double)n;
-        int layer = (int)(pct * kLayers) + 1;
-        if (layer > kLayers) layer = kLayers;
-        const int l = layer - 1;
-        if (vx == vx) {
-            lcnt[l] += 1;
-            const double y = vx - lcomp[l];
-            const double tt = lsum[l] + y;
-            lcomp[l] = tt - lsum[l] - y;
-            if (lcomp[l] != lcomp[l]) lcomp[l] = 0;
-            lsum[l] = tt;
+        __syncthreads();
+        if (wave == 0 && lane < 3) {
+            const double* R = sv[1 + k0];
+            for (int e = 0; e < len; ++e) {
+                const double vy = sv[0][e], vx = R[e];
+                if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
+                    nobs += 1;
+                    const double dx = vx - mx, dy = vy - my;
+                    mx += 1. / nobs * dx;
+                    my += 1. / nobs * dy;
+                    sxx += (vx - mx) * dx;
+                    syy += (vy - my) * dy;
+                    sxy += (vx - mx) * dy;
+                }
+            }
+        } else if (wave == 1 && lane < 3 * kLayers) {
+            const double* R = sv[1 + k1];
+            for (int e = 0; e < len; ++e) {
+                const double vx = R[e];
+                if (slay[e] == l1 && vx == vx) {
+                    lcnt += 1;
+                    const double y = vx - lcomp;
+                    const double tt = lsum + y;
+                    lcomp = tt - lsum - y;
+                    if (lcomp != lcomp) lcomp = 0;
+                    lsum = tt;
+                }
+            }
         }
-        const int rd = g.rank_desc[base + e];
-        if (rd <= kTopK) {
-            pv_f[rd - 1] = vy;
-            pv_r[rd - 1] = vx;
-            pv_has[rd - 1] = true;
+    }
+    __syncthreads();
+    if (wave == 1 && lane < 3 * kLayers) {
+        g.layer_mean[(di * 3 + k1) * kLayers + l1] = lcnt ? lsum / (double)lcnt : qnan();
+        if (k1 == 0) g.layer_cnt[di * kLayers + l1] = lcnt;
+    }
+    if (wave == 0 && lane < 3) {
+        const int k = k0;
+        double r = qnan();
+        if (nobs >= 1) {
+            const double div = __builtin_sqrt(sxx * syy);
+            if (div != 0) r = sxy / div;
         }
+        g.ic[di * 3 + k] = r;
+        // pivot columns in string order '1.0','10.0','2.0',...,'9.0' (or 1..m for m < 10)
+        int order[kTopK];
+        const int m = g.mcols;
+        if (m >= 10) {
+            order[0] = 1; order[1] = 10;
+            for (int j = 2; j < 10; ++j) order[j] = j;
+        } else {
+            for (int j = 0; j < m; ++j) order[j] = j + 1;
+        }
+        double row[kTopK];
+        for (int j = 0; j < m; ++j) {
+            const double f = pv_has[order[j] - 1] ? pv_f[order[j] - 1] : qnan();
+            row[j] = f == f ? f : 0.0;
+        }
+        const double wsum = leaf_sum(row, m);
+        for (int j = 0; j < m; ++j) {
+            const int q = order[j] - 1;
+            double v = qnan();
+            if (pv_has[q]) v = pv_r[k][q] * (pv_f[q] / wsum);
+            row[j] = v == v ? v : 0.0;
+        }
+        g.port[di * 3 + k] = leaf_sum(row, m);
     }
-    double r = qnan();
-    if (nobs >= 1) {
-        const double div = __builtin_sqrt(sxx * syy);
-        if (div != 0) r = sxy / div;
-    }
-    g.ic[di * 3 + k] = r;
-    for (int l = 0; l < kLayers; ++l) {
-        g.layer_mean[(di * 3 + k) * kLayers + l] = lcnt[l] ? lsum[l] / (double)lcnt[l] : qnan();
-        if (k == 0) g.layer_cnt[di * kLayers + l] = lcnt[l];
-    }
-    // pivot columns in string order '1.0','10.0','2.0',...,'9.0' (or 1..m for m < 10)
-    int order[kTopK];
-    int m = g.mcols;
-    if (m >= 10) {
-        order[0] = 1; order[1] = 10;
-        for (int j = 2; j < 10; ++j) order[j] = j;
-    } else {
-        for (int j = 0; j < m; ++j) order[j] = j + 1;
-    }
-    double row[kTopK];
-    for (int j = 0; j < m; ++j) {
-        const double f = pv_has[order[j] - 1] ? pv_f[order[j] - 1] : qnan();
-        row[j] = f == f ? f : 0.0;
-    }
-    const double wsum = leaf_sum(row, m);
-    for (int j = 0; j < m; ++j) {
-        const int q = order[j] - 1;
-        double v = qnan();
-        if (pv_has[q]) v = pv_r[q] * (pv_f[q] / wsum);
-        row[j] = v == v ? v : 0.0;
-    }
-    g.port[di * 3 + k] = leaf_sum(row, m);
 }
 
 // ---- series: cumulative layers / long-short / top-k, per-year IR -----------------------------
@@ -604,7 +655,18 @@ extern "C" int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const doubl
     AFM_CHECK_ARG(T > 0 && lda % 64 == 0, "bad shape");
     AFM_CHECK_ARG(rows && nrows && skey && sidx && rank_asc && rank_desc, "null buffer");
     RankArgs g{T, lda, rows, nrows, (u64*)skey, sidx, rank_asc, rank_desc};
-    hipLaunchKernelGGL(xs_rank_kernel, dim3((unsigned)T), dim3(kT), 0, ctx->stream, g);
+    // phase-2 LDS: 12 B per row, up to 144 KB (a date with more rows searches in global memory)
+    const size_t sort_bytes = (sizeof(u64) + sizeof(int32_t)) * kChunk;
+    int lds_rows = (int)(lda < 12288 ? lda : 12288);
+    const size_t lds = std::max(sort_bytes, (size_t)lds_rows * 12);
+    static bool attr = false;
+    if (!attr) {
+        AFM_HIP(hipFuncSetAttribute((const void*)xs_rank_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 12288 * 12));
+        attr = true;
+    }
+    hipLaunchKernelGGL(xs_rank_kernel, dim3((unsigned)T), dim3(kT), lds, ctx->stream, g,
+                       lds_rows);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
@@ -621,8 +683,7 @@ extern "C" int afm_xs_stats_f64(afm_ctx* ctx, int64_t T, int64_t lda, const int3
     if (nd <= 0) return AFM_OK;
     StatArgs g{T, lda, dates, nd, rows, nrows, rank_asc, rank_desc, mcols, ic, layer_mean,
                layer_cnt, port};
-    hipLaunchKernelGGL(xs_stats_kernel, dim3((unsigned)((nd * 3 + 63) / 64)), dim3(64), 0,
-                       ctx->stream, g);
+    hipLaunchKernelGGL(xs_stats_kernel, dim3((unsigned)nd), dim3(128), 0, ctx->stream, g);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

@@ -25,6 +25,8 @@
 // row from HBM (+16 p per row of {mu, 1/sigma}, L2-resident per asset block: blocks map to XCDs).
 #include "afm_internal.h"
 
+#include <cstdlib>
+
 #pragma clang fp contract(off)
 
 namespace afm {
@@ -32,6 +34,9 @@ namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 typedef unsigned long long u64;
+// LDS-qualified double: keeps ring accesses on ds_read / ds_write (a generic pointer to dynamic
+// LDS would compile to flat loads, which wait on vmcnt and lgkmcnt together)
+typedef __attribute__((address_space(3))) double lds_double;
 
 constexpr int kZRS = 66;                     // LDS row stride (doubles): conflict-free fragments
 constexpr int kZMaxSlots = 3;                // ring depth (2 when p + 4 staged rows do not fit 3x)
@@ -88,7 +93,7 @@ struct ZGramArgs {
 // fragment source of the padding features, row p+3: dump row of the dummy columns), dynamic
 // LDS; counters in static LDS.
 struct ZSmem {
-    double* tile;            // [nslots][p + 4][kZRS]
+    lds_double* tile;        // [nslots][p + 4][kZRS]
     int slot_elems;          // (p + 4) * kZRS
     int nslots;
     int ready[kZMaxSlots];
@@ -166,8 +171,13 @@ struct Seq {
 // ahead, issued before the newer x loads (loads retire in order); mode 1 once per item -- the
 // item keeps its 64 assets, so the row-block's statistics stay in registers across its dates.
 // z = (x - mu) * rsig; masked-out rows stage exact zeros.
-template <int NT, int MODE>
-__device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int pw, const int lane) {
+#ifndef AFM_ZG_TPL
+#define AFM_ZG_TPL 0
+#endif
+template <int NT, int MODE, int PW>
+__device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, const int pw_rt) {
+    // AFM_ZG_TPL: the wave index as a compile-time constant (immediate LDS offsets) or not
+    const int pw = AFM_ZG_TPL ? PW : pw_rt;
     constexpr int MC = ZCfg<NT>::MC;
     const int p = g.p;
     const int K = p + 2;
@@ -194,7 +204,6 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int pw, const
         asm volatile("" : "+s"(q));
         return (unsigned)((q >> 16) * lda) * 16u;
     };
-    const bool ones = pw == 0;               // column j = 0 of wave 0 is the ones column
     const char* zb = reinterpret_cast<const char*>(g.zs);
     struct Buf {
         double x[MC];
@@ -241,13 +250,13 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int pw, const
             zitem = B.item;
         }
         wait_count(&sm.freed[slot], ZCfg<NT>::NCW * gen);
-        double* tb = sm.tile + slot * sm.slot_elems + lane;
+        lds_double* tb = sm.tile + slot * sm.slot_elems + lane;
 #pragma unroll
         for (int j = 0; j < MC; ++j) {
             const int k = pw + kZProd * j;
             const int lrow = k < K ? k : p + 3;      // the dump row takes the dummy columns
             double v = (B.x[j] - mu[j]) * rs[j];     // y: identity row {0, 1}
-            if (j == 0) v = ones ? 1.0 : v;
+            if (k == 0) v = 1.0;                     // the ones column (wave 0, j = 0)
             tb[lrow * kZRS] = B.ok ? v : 0.0;
         }
         signal_count(&sm.ready[slot], lane);
@@ -295,7 +304,7 @@ __device__ void zgram_consume(const ZGramArgs& g, ZSmem& sm, const int lane) {
     Seq cur;
     for (cur.init(g); cur.valid(); cur.advance(g)) {
         wait_count(&sm.ready[slot], kZProd * gen);
-        const double* tb = sm.tile + slot * sm.slot_elems;
+        const lds_double* tb = sm.tile + slot * sm.slot_elems;
         double fa[NT], fb[NT];
         auto ld = [&](double (&f)[NT], int it) {
             const int a = it * 4 + kk;
@@ -311,13 +320,27 @@ __device__ void zgram_consume(const ZGramArgs& g, ZSmem& sm, const int lane) {
                 acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[tab.I[Q0 + q]], f[tab.J[Q0 + q]],
                                                               acc[q], 0, 0, 0);
         };
+        // k-step it+1's fragments are requested before k-step it's MFMAs (the sched barriers keep
+        // that order, so each wait covers only the older requests)
+#ifndef AFM_ZG_SB
+#define AFM_ZG_SB 0
+#endif
+#if AFM_ZG_SB
+#define ZG_SB() __builtin_amdgcn_sched_barrier(0)
+#else
+#define ZG_SB()
+#endif
         ld(fa, 0);
 #pragma unroll
         for (int it = 0; it < 16; it += 2) {
             ld(fb, it + 1);
+            ZG_SB();
             step(fa);
+            ZG_SB();
             if (it + 2 < 16) ld(fa, it + 2);
+            ZG_SB();
             step(fb);
+            ZG_SB();
         }
         signal_count(&sm.freed[slot], lane);
         if (++slot == sm.nslots) { slot = 0; ++gen; }
@@ -334,7 +357,7 @@ __device__ void zgram_consume(const ZGramArgs& g, ZSmem& sm, const int lane) {
 }
 
 template <int NT, int MODE>
-__global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int nslots) {
+__global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int nslots, int prio) {
     extern __shared__ __attribute__((aligned(16))) double ring[];
     __shared__ ZSmem sm;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -342,13 +365,33 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
     const int se = (g.p + 4) * kZRS;
     // zero the ring once: the zero row (p + 2) is never written afterwards
     for (int i = tid; i < nslots * se; i += kZThreads) ring[i] = 0.0;
-    if (tid == 0) { sm.tile = ring; sm.slot_elems = se; sm.nslots = nslots; }
+    if (tid == 0) {
+        sm.tile = (lds_double*)ring;
+        sm.slot_elems = se;
+        sm.nslots = nslots;
+    }
     if (tid < kZMaxSlots) { sm.ready[tid] = 0; sm.freed[tid] = 0; }
     __syncthreads();
     if (wave >= 4) {
-        __builtin_amdgcn_s_setprio(1);
-        zgram_produce<NT, MODE>(g, sm, wave - 4, lane);
-    } else if (wave == 0) {
+        if (prio & 1) __builtin_amdgcn_s_setprio(1);
+        if (!AFM_ZG_TPL) {
+            zgram_produce<NT, MODE, 0>(g, sm, lane, wave - 4);
+        } else {
+            switch (wave - 4) {
+                case 0: zgram_produce<NT, MODE, 0>(g, sm, lane, 0); break;
+                case 1: zgram_produce<NT, MODE, 1>(g, sm, lane, 1); break;
+                case 2: zgram_produce<NT, MODE, 2>(g, sm, lane, 2); break;
+                case 3: zgram_produce<NT, MODE, 3>(g, sm, lane, 3); break;
+                case 4: zgram_produce<NT, MODE, 4>(g, sm, lane, 4); break;
+                case 5: zgram_produce<NT, MODE, 5>(g, sm, lane, 5); break;
+                case 6: zgram_produce<NT, MODE, 6>(g, sm, lane, 6); break;
+                default: zgram_produce<NT, MODE, 7>(g, sm, lane, 7); break;
+            }
+        }
+        return;
+    }
+    if (prio & 2) __builtin_amdgcn_s_setprio(2);
+    if (wave == 0) {
         zgram_consume<NT, 0>(g, sm, lane);
     } else if constexpr (ZCfg<NT>::NCW == 4) {
         if (wave == 1) zgram_consume<NT, 1>(g, sm, lane);
@@ -487,8 +530,14 @@ static int launch_zgram(afm_ctx* ctx, const ZGramArgs& g, int64_t nitems, int gr
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kZLds));
         attr = true;
     }
+    // AFM_ZG_PRIO (experiments): bit 0 = producers at priority 1 (default), bit 1 = consumers at 2
+    static int prio = -1;
+    if (prio < 0) {
+        const char* e = getenv("AFM_ZG_PRIO");
+        prio = e ? atoi(e) : 1;
+    }
     hipLaunchKernelGGL((zgram_kernel<NT, MODE>), dim3((unsigned)wg), dim3(kZThreads),
-                       (size_t)nslots * slot_bytes, ctx->stream, g, nslots);
+                       (size_t)nslots * slot_bytes, ctx->stream, g, nslots, prio);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
