@@ -25,10 +25,11 @@ One ``step()`` over a device-resident calendar-grid panel:
 side streams:
 8. analyzer     AlphaSignalAnalyzer(lasso_predict, price_data=df_test close).run() (KKT:630-631):
                 forward returns, IC, decile layers, top-10 backtest, IR
-9. fm           the north-star extension: per-date Grams of [1, FM30 z-scores,
-                target] (afm_zgram_f64: per (date, asset block) partials, fixed tree), per-date
-                cross-sectional OLS + Fama-MacBeth mean / t.  FM30 is a stated well-conditioned
-                subset of the 97 features.
+9. fm           the north-star extension: classic Fama-MacBeth -- per-date Grams of
+                [1, FM30 factor values, target] over the same rows (afm_zgram_f64: per (date,
+                asset block) partials, fixed tree), per-date cross-sectional OLS, mean / t.
+                FM30 is a stated well-conditioned subset of the 97 features (worst date
+                cond(corr) ~3e2 on config A, raw or z-scored).
 
 The reference's LinearRegression over all 97 columns (KKT:582-583) is not a stage: that design
 is numerically rank-deficient (cond ~1e10 measured on config A: BBANDS_upper + BBANDS_lower =
@@ -135,8 +136,6 @@ class Pipeline:
         i64 = dict(dtype=torch.int64, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         self.feat = torch.as_tensor(np.array([COL[n] for n in FEATURES], np.int32), device=dev)
-        self.fm_sel = torch.as_tensor(np.array([FEATURES.index(n) for n in c.fm_features],
-                                               np.int32), device=dev)   # their zs rows
         self.pf = len(c.fm_features)
         self.out = torch.full((N_FACTORS, T, lda), float("nan"), **f64)
         self.nanfree = torch.zeros((nch, lda), **i64)
@@ -267,9 +266,9 @@ class Pipeline:
         """Per-date FM30 Grams, solves and Fama-MacBeth statistics."""
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
         T, lda, p, pf, c = self.T, self.lda, self.p, self.pf, self.cfg
-        chk(L.afm_zgram_f64(h, P(self.out), T * lda, lda, P(self.fm_cols), P(self.fm_sel), pf,
-                            TARGET, P(self.zs), p, P(self.zrows), 0, T, self.nblk, 0, self.blk,
-                            self.A, P(self.fm_part), 0), "zgram fm")
+        chk(L.afm_zgram_f64(h, P(self.out), T * lda, lda, P(self.fm_cols), None, pf, TARGET,
+                            None, 0, P(self.zrows), 0, T, self.nblk, 0, self.blk, self.A,
+                            P(self.fm_part), 0), "zgram fm")
         chk(L.afm_gram_tree_f64(h, pf, P(self.fm_part), T * self.nblk, self.nblk, 1,
                                 P(self.fm_gram)), "tree fm")
         chk(L.afm_ols_solve_f64(h, P(self.fm_gram), P(self.fm_shift), pf, T, c.tol,

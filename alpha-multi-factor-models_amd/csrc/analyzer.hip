@@ -29,6 +29,7 @@ namespace {
 
 typedef unsigned long long u64;
 constexpr int kT = 256;
+constexpr int kWT = 1024;              // per-date analyzer kernels: 16 waves (latency hiding)
 constexpr int kChunk = 2048;          // rows per LDS-sorted chunk
 constexpr int kMaxLeaves = 1024;      // pairwise leaves (n <= 65536)
 constexpr int kTopK = 10;
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(256) void fwd_returns_kernel(int64_t T, int64_t lda
 // ---- block helpers ---------------------------------------------------------------------------
 // exclusive scan of 0/1 flags over the 256 threads: ballots within the waves, wave totals
 // through LDS (two barriers instead of a log-step scan)
+template <int NT = kT>
 __device__ int block_scan(int v, int* sbuf, int* excl) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const u64 m = __ballot(v != 0);
@@ -94,7 +96,7 @@ __device__ int block_scan(int v, int* sbuf, int* excl) {
     __syncthreads();
     int off = 0, total = 0;
 #pragma unroll
-    for (int i = 0; i < kT / 64; ++i) {
+    for (int i = 0; i < NT / 64; ++i) {
         off += i < w ? sbuf[i] : 0;
         total += sbuf[i];
     }
@@ -151,6 +153,7 @@ __device__ double leaf_sum(const double* a, int n) {
 }
 
 // np.add.reduce of v[0..n) (0.0 + numpy pairwise sum), evaluated by the whole block
+template <int NT = kT>
 __device__ double block_np_sum(PwShared& p, const double* v, int64_t n) {
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -159,7 +162,7 @@ __device__ double block_np_sum(PwShared& p, const double* v, int64_t n) {
         if (n > 0) pw_enum(p, 0, n);
     }
     __syncthreads();
-    for (int l = tid; l < p.nleaves; l += kT) p.lval[l] = leaf_sum(v + p.loff[l], p.llen[l]);
+    for (int l = tid; l < p.nleaves; l += NT) p.lval[l] = leaf_sum(v + p.loff[l], p.llen[l]);
     __syncthreads();
     if (tid == 0) p.result = n > 0 ? 0.0 + pw_combine(p, n) : 0.0;
     __syncthreads();
@@ -179,9 +182,9 @@ struct PrepArgs {
     int32_t* nrows;           // [T] surviving rows per date
 };
 
-__global__ __launch_bounds__(kT) void xs_prepare_kernel(PrepArgs g) {
+__global__ __launch_bounds__(kWT) void xs_prepare_kernel(PrepArgs g) {
     __shared__ PwShared pw;
-    __shared__ int sbuf[kT];
+    __shared__ int sbuf[kWT / 64];
     const int tid = threadIdx.x;
     const int64_t t = blockIdx.x;
     const int64_t plane = g.T * g.lda;
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(kT) void xs_prepare_kernel(PrepArgs g) {
     for (int k = 0; k < 3; ++k) {
         // rows surviving step k: signal and returns 1..k all present
         int n = 0;
-        for (int64_t base = 0; base < g.A; base += kT) {
+        for (int64_t base = 0; base < g.A; base += kWT) {
             const int64_t a = base + tid;
             int ok = 0;
             double v = 0.0;
@@ -204,16 +207,16 @@ __global__ __launch_bounds__(kT) void xs_prepare_kernel(PrepArgs g) {
                 v = g.fr[k * plane + t * g.lda + a];
             }
             int ex;
-            const int tot = block_scan(ok, sbuf, &ex);
+            const int tot = block_scan<kWT>(ok, sbuf, &ex);
             if (ok) scr[n + ex] = v;
             n += tot;
         }
         __syncthreads();
-        mu[k] = n > 0 ? block_np_sum(pw, scr, n) / (double)n : qnan();
+        mu[k] = n > 0 ? block_np_sum<kWT>(pw, scr, n) / (double)n : qnan();
     }
     // final rows (all three returns), compacted with demeaned returns
     int n = 0;
-    for (int64_t base = 0; base < g.A; base += kT) {
+    for (int64_t base = 0; base < g.A; base += kWT) {
         const int64_t a = base + tid;
         int ok = 0;
         if (a < g.A) {
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(kT) void xs_prepare_kernel(PrepArgs g) {
             }
         }
         int ex;
-        const int tot = block_scan(ok, sbuf, &ex);
+        const int tot = block_scan<kWT>(ok, sbuf, &ex);
         if (ok) {
             const int64_t o = t * g.lda + n + ex;
             g.rows[o] = sig[a];
@@ -247,7 +250,7 @@ struct RankArgs {
     int32_t* rank_desc;       // [T][lda]
 };
 
-__global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g, int lds_rows) {
+__global__ __launch_bounds__(kWT) void xs_rank_kernel(RankArgs g, int lds_rows) {
     // dynamic LDS: phase 1 the sort buffers, phase 2 (n <= lds_rows) the date's sorted chunks
     extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
     u64* key = reinterpret_cast<u64*>(dyn);
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g, int lds_rows) {
     const int nch = (n + kChunk - 1) / kChunk;
     for (int c = 0; c < nch; ++c) {
         const int c0 = c * kChunk, len = min(kChunk, n - c0);
-        for (int e = tid; e < kChunk; e += kT) {
+        for (int e = tid; e < kChunk; e += kWT) {
             if (e < len) {
                 key[e] = okey(g.rows[base + c0 + e]);
                 idx[e] = c0 + e;
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g, int lds_rows) {
         // bitonic sort of (key, idx) ascending
         for (int size = 2; size <= kChunk; size <<= 1) {
             for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                for (int e = tid; e < kChunk / 2; e += kT) {
+                for (int e = tid; e < kChunk / 2; e += kWT) {
                     const int lo = 2 * e - (e & (stride - 1));
                     const int hi = lo + stride;
                     const bool up = ((lo & size) == 0);
@@ -287,7 +290,7 @@ __global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g, int lds_rows) {
                 __syncthreads();
             }
         }
-        for (int e = tid; e < len; e += kT) {
+        for (int e = tid; e < len; e += kWT) {
             g.skey[base + c0 + e] = key[e];
             g.sidx[base + c0 + e] = idx[e];
         }
@@ -299,13 +302,13 @@ __global__ __launch_bounds__(kT) void xs_rank_kernel(RankArgs g, int lds_rows) {
     u64* LK = reinterpret_cast<u64*>(dyn);
     int32_t* LI = reinterpret_cast<int32_t*>(dyn + sizeof(u64) * (size_t)lds_rows);
     if (in_lds && nch > 1) {
-        for (int e = tid; e < n; e += kT) {
+        for (int e = tid; e < n; e += kWT) {
             LK[e] = g.skey[base + e];
             LI[e] = g.sidx[base + e];
         }
         __syncthreads();
     }
-    for (int e = tid; e < n; e += kT) {
+    for (int e = tid; e < n; e += kWT) {
         const u64 k0 = okey(g.rows[base + e]);
         int less = 0, greater = 0;
         for (int c = 0; c < nch; ++c) {
@@ -643,7 +646,7 @@ extern "C" int afm_xs_prepare_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t ld
     AFM_CHECK_ARG(T > 0 && A > 0 && lda >= A && lda % 64 == 0 && A <= 65536, "bad shape");
     AFM_CHECK_ARG(sig && fr && scratch && rows && rows_idx && nrows, "null buffer");
     PrepArgs g{T, lda, A, sig, fr, scratch, rows, rows_idx, nrows};
-    hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)T), dim3(kT), 0, ctx->stream, g);
+    hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)T), dim3(kWT), 0, ctx->stream, g);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
@@ -665,7 +668,7 @@ extern "C" int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const doubl
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 12288 * 12));
         attr = true;
     }
-    hipLaunchKernelGGL(xs_rank_kernel, dim3((unsigned)T), dim3(kT), lds, ctx->stream, g,
+    hipLaunchKernelGGL(xs_rank_kernel, dim3((unsigned)T), dim3(kWT), lds, ctx->stream, g,
                        lds_rows);
     AFM_HIP(hipGetLastError());
     return AFM_OK;

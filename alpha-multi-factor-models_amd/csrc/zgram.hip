@@ -51,7 +51,7 @@ template <int NT>
 struct ZCfg {
     static constexpr int NP = NT * (NT + 1) / 2;
     static constexpr int PE = NP * 256;                        // doubles of one partial
-    static constexpr int NCW = NT == 7 ? 4 : 1;                // consumer waves
+    static constexpr int NCW = NT == 7 ? 4 : 3;                // consumer waves
     static constexpr int PPW = (NP + NCW - 1) / NCW;           // pairs per consumer wave
     static constexpr int KMAX = NT == 7 ? 108 : 16 * NT;       // staged columns p + 2 <= KMAX
     static constexpr int MC = (KMAX + kZProd - 1) / kZProd;    // columns per producer wave
@@ -174,7 +174,7 @@ struct Seq {
 #ifndef AFM_ZG_TPL
 #define AFM_ZG_TPL 0
 #endif
-template <int NT, int MODE, int PW>
+template <int NT, int MODE, bool ZS, int PW>
 __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, const int pw_rt) {
     // AFM_ZG_TPL: the wave index as a compile-time constant (immediate LDS offsets) or not
     const int pw = AFM_ZG_TPL ? PW : pw_rt;
@@ -236,6 +236,7 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, con
 #if defined(AFM_ZG_SKIP) && AFM_ZG_SKIP == 2
         return;
 #endif
+        if (!ZS) return;                             // raw columns: no statistics
 #pragma unroll
         for (int j = 0; j < MC; ++j) {
             const double2 m = *reinterpret_cast<const double2*>(zb + zsrc(j) + zoff);
@@ -245,7 +246,7 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, con
     };
     int slot = 0, gen = 0;
     auto stage = [&](const Buf& B) {
-        if (MODE == 1 && B.item != zitem) {          // a new item: its row-block's statistics
+        if (ZS && MODE == 1 && B.item != zitem) {    // a new item: its row-block's statistics
             zload(B.zoff);
             zitem = B.item;
         }
@@ -255,7 +256,7 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, con
         for (int j = 0; j < MC; ++j) {
             const int k = pw + kZProd * j;
             const int lrow = k < K ? k : p + 3;      // the dump row takes the dummy columns
-            double v = (B.x[j] - mu[j]) * rs[j];     // y: identity row {0, 1}
+            double v = ZS ? (B.x[j] - mu[j]) * rs[j] : B.x[j];   // y: identity row {0, 1}
             if (k == 0) v = 1.0;                     // the ones column (wave 0, j = 0)
             tb[lrow * kZRS] = B.ok ? v : 0.0;
         }
@@ -356,7 +357,7 @@ __device__ void zgram_consume(const ZGramArgs& g, ZSmem& sm, const int lane) {
     }
 }
 
-template <int NT, int MODE>
+template <int NT, int MODE, bool ZS>
 __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int nslots, int prio) {
     extern __shared__ __attribute__((aligned(16))) double ring[];
     __shared__ ZSmem sm;
@@ -375,17 +376,17 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
     if (wave >= 4) {
         if (prio & 1) __builtin_amdgcn_s_setprio(1);
         if (!AFM_ZG_TPL) {
-            zgram_produce<NT, MODE, 0>(g, sm, lane, wave - 4);
+            zgram_produce<NT, MODE, ZS, 0>(g, sm, lane, wave - 4);
         } else {
             switch (wave - 4) {
-                case 0: zgram_produce<NT, MODE, 0>(g, sm, lane, 0); break;
-                case 1: zgram_produce<NT, MODE, 1>(g, sm, lane, 1); break;
-                case 2: zgram_produce<NT, MODE, 2>(g, sm, lane, 2); break;
-                case 3: zgram_produce<NT, MODE, 3>(g, sm, lane, 3); break;
-                case 4: zgram_produce<NT, MODE, 4>(g, sm, lane, 4); break;
-                case 5: zgram_produce<NT, MODE, 5>(g, sm, lane, 5); break;
-                case 6: zgram_produce<NT, MODE, 6>(g, sm, lane, 6); break;
-                default: zgram_produce<NT, MODE, 7>(g, sm, lane, 7); break;
+                case 0: zgram_produce<NT, MODE, ZS, 0>(g, sm, lane, 0); break;
+                case 1: zgram_produce<NT, MODE, ZS, 1>(g, sm, lane, 1); break;
+                case 2: zgram_produce<NT, MODE, ZS, 2>(g, sm, lane, 2); break;
+                case 3: zgram_produce<NT, MODE, ZS, 3>(g, sm, lane, 3); break;
+                case 4: zgram_produce<NT, MODE, ZS, 4>(g, sm, lane, 4); break;
+                case 5: zgram_produce<NT, MODE, ZS, 5>(g, sm, lane, 5); break;
+                case 6: zgram_produce<NT, MODE, ZS, 6>(g, sm, lane, 6); break;
+                default: zgram_produce<NT, MODE, ZS, 7>(g, sm, lane, 7); break;
             }
         }
         return;
@@ -393,10 +394,12 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
     if (prio & 2) __builtin_amdgcn_s_setprio(2);
     if (wave == 0) {
         zgram_consume<NT, 0>(g, sm, lane);
+    } else if (wave == 1) {
+        zgram_consume<NT, 1>(g, sm, lane);
+    } else if (wave == 2) {
+        zgram_consume<NT, 2>(g, sm, lane);
     } else if constexpr (ZCfg<NT>::NCW == 4) {
-        if (wave == 1) zgram_consume<NT, 1>(g, sm, lane);
-        else if (wave == 2) zgram_consume<NT, 2>(g, sm, lane);
-        else zgram_consume<NT, 3>(g, sm, lane);
+        zgram_consume<NT, 3>(g, sm, lane);
     }
 }
 
@@ -515,7 +518,7 @@ extern "C" int afm_zgram_part_bytes(int p) {
     return (int)sizeof(double) * (zgram_nt(p) == 2 ? ZCfg<2>::PE : ZCfg<7>::PE);
 }
 
-template <int NT, int MODE>
+template <int NT, int MODE, bool ZS>
 static int launch_zgram(afm_ctx* ctx, const ZGramArgs& g, int64_t nitems, int grid) {
     int64_t wg = grid > 0 ? grid : 256;                 // persistent: one workgroup per CU
     if (wg > nitems) wg = nitems;
@@ -526,7 +529,7 @@ static int launch_zgram(afm_ctx* ctx, const ZGramArgs& g, int64_t nitems, int gr
     AFM_CHECK_ARG(nslots >= 2, "ring does not fit in LDS");
     static bool attr = false;
     if (!attr) {
-        AFM_HIP(hipFuncSetAttribute((const void*)zgram_kernel<NT, MODE>,
+        AFM_HIP(hipFuncSetAttribute((const void*)zgram_kernel<NT, MODE, ZS>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kZLds));
         attr = true;
     }
@@ -536,7 +539,7 @@ static int launch_zgram(afm_ctx* ctx, const ZGramArgs& g, int64_t nitems, int gr
         const char* e = getenv("AFM_ZG_PRIO");
         prio = e ? atoi(e) : 1;
     }
-    hipLaunchKernelGGL((zgram_kernel<NT, MODE>), dim3((unsigned)wg), dim3(kZThreads),
+    hipLaunchKernelGGL((zgram_kernel<NT, MODE, ZS>), dim3((unsigned)wg), dim3(kZThreads),
                        (size_t)nslots * slot_bytes, ctx->stream, g, nslots, prio);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
@@ -545,7 +548,7 @@ static int launch_zgram(afm_ctx* ctx, const ZGramArgs& g, int64_t nitems, int gr
 static int zgram_common_checks(const double* base, const int32_t* cols, const double* zs,
                                const uint64_t* bits, double* part, int p, int64_t lda,
                                int64_t a_end, int64_t blk0, int64_t t0, int64_t nt) {
-    AFM_CHECK_ARG(base && cols && zs && bits && part, "null buffer");
+    AFM_CHECK_ARG(base && cols && bits && part, "null buffer");
     AFM_CHECK_ARG(p >= 1 && p + 2 <= ZCfg<7>::KMAX, "need 1 <= p <= 106");
     AFM_CHECK_ARG(lda > 0 && lda % 64 == 0 && a_end <= lda, "lda must be a multiple of 64 >= a_end");
     AFM_CHECK_ARG(blk0 >= 0 && blk0 % 64 == 0, "blk0 must be a multiple of 64");
@@ -568,8 +571,9 @@ extern "C" int afm_zgram_f64(afm_ctx* ctx, const double* base, int64_t col_strid
     if (nt == 0) return AFM_OK;
     ZGramArgs g{base, col_stride, lda, cols, zcols, p, ycol, zid, zs, bits, t0, nt, 0, nblk, blk0,
                 blk_assets, a_end, 0, 1, part};
-    return zgram_nt(p) == 2 ? launch_zgram<2, 0>(ctx, g, nt * nblk, grid)
-                            : launch_zgram<7, 0>(ctx, g, nt * nblk, grid);
+    if (!zs) return launch_zgram<2, 0, false>(ctx, g, nt * nblk, grid);   // FM: raw columns
+    return zgram_nt(p) == 2 ? launch_zgram<2, 0, true>(ctx, g, nt * nblk, grid)
+                            : launch_zgram<7, 0, true>(ctx, g, nt * nblk, grid);
 }
 
 extern "C" int afm_zpool_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
@@ -584,8 +588,9 @@ extern "C" int afm_zpool_f64(afm_ctx* ctx, const double* base, int64_t col_strid
     if (nrb == 0) return AFM_OK;
     ZGramArgs g{base, col_stride, lda, cols, zcols, p, ycol, zid, zs, bits, t0, nt, 1, 1, blk0,
                 64, a_end, nrb, nchunk, part};
-    return zgram_nt(p) == 2 ? launch_zgram<2, 1>(ctx, g, (int64_t)nrb * nchunk, grid)
-                            : launch_zgram<7, 1>(ctx, g, (int64_t)nrb * nchunk, grid);
+    AFM_CHECK_ARG(zs != nullptr, "afm_zpool_f64 needs zs");
+    return zgram_nt(p) == 2 ? launch_zgram<2, 1, true>(ctx, g, (int64_t)nrb * nchunk, grid)
+                            : launch_zgram<7, 1, true>(ctx, g, (int64_t)nrb * nchunk, grid);
 }
 
 extern "C" int afm_gram_tree_f64(afm_ctx* ctx, int p, const double* in, int64_t total, int per,

@@ -267,7 +267,8 @@ int afm_row_bits(afm_ctx* ctx, int64_t nch, int64_t lda, const uint64_t* a, cons
 int afm_zgram_part_bytes(int p);
 /* Partial Grams of Z = [1, z_1..z_p, y] on fp64 MFMA (v_mfma_f64_16x16x4_f64), z_j = (x_j - mu)
  * * (1/sd) with {mu, 1/sd} = zs row zcols[j] (DEVICE int32; NULL = row j), y = plane ycol scaled
- * by zs row zid (the identity row of afm_zstats_finalize_f64); rows = set bits of `bits`;
+ * by zs row zid (the identity row of afm_zstats_finalize_f64); zs = NULL (afm_zgram_f64 only):
+ * raw columns, no scaling; rows = set bits of `bits`;
  * regressor j is plane cols[j].  1 <= p <= 106; grid = workgroups (0: one per CU).
  * afm_zgram_f64 -- one partial per (date, asset block): dates [t0, t0+nt), block b = assets
  *   [blk0 + b*blk_assets, + blk_assets) below a_end; part [nt][nblk][part].  The per-date Grams

@@ -13,8 +13,8 @@ feed ``PortfolioManager`` in the reference:
 * portfolio          KKT:976-977: oracle.portfolio.run_portfolio (exact box-QP in place of SLSQP,
                      SURVEY F6), history = target on the z-score-surviving rows, rolling window
 * analyzer           KKT:630-631: oracle.xs.analyze on the test predictions and df_test closes
-* Fama-MacBeth       the north-star per-date OLS: numpy lstsq per date on the FM
-                     columns of the same z-scored rows, oracle.pipeline.fama_macbeth
+* Fama-MacBeth       the north-star per-date OLS: numpy lstsq per date of the target
+                     on the raw FM factor columns of the same rows, oracle.pipeline.fama_macbeth
 
 Inputs are a synthetic ``Panel`` (afm.synthetic); outputs are long arrays in (date, id) order.
 """
@@ -91,9 +91,9 @@ def run_chain(p, train_end="2015-12-31", valid_end="2016-12-31", *, alpha=2e-4, 
         tm["analyzer"] = time.perf_counter() - t4
     if fm and len(fm_features):
         t5 = time.perf_counter()
-        fj = [FEATURES.index(n) for n in fm_features]
+        fj = [FACTOR_NAMES.index(n) for n in fm_features]      # raw factor values
         rows = np.flatnonzero(zr)
-        d, B, N = PL.xs_ols(tt[rows], Z[rows][:, fj], y[rows])
+        d, B, N = PL.xs_ols(tt[rows], fac[rows][:, fj], y[rows])
         res["fm_dates"], res["fm_beta"], res["fm_n"] = d, B, N
         tm["fm"] = time.perf_counter() - t5
     return res

@@ -80,8 +80,12 @@ def xs_ols(date: np.ndarray, X: np.ndarray, y: np.ndarray):
     for g in range(len(off) - 1):
         s, e = off[g], off[g + 1]
         A = np.column_stack([np.ones(e - s), X[s:e]])
-        beta, *_ = np.linalg.lstsq(A, y[s:e], rcond=None)
-        B.append(beta)
+        # equilibrated columns (raw factors span ~1e9 in scale: an unscaled lstsq loses the
+        # small columns' digits), solved, then unscaled
+        sc = np.sqrt((A * A).sum(axis=0))
+        sc[sc == 0] = 1.0
+        beta, *_ = np.linalg.lstsq(A / sc, y[s:e], rcond=None)
+        B.append(beta / sc)
         N.append(e - s)
     return date[off[:-1]], np.array(B), np.array(N)
 
