@@ -64,11 +64,13 @@ FM30 = ["tmr_ret1d", "ACCEL_32", "sd5_15", "corr_5", "OBV", "sd_15", "MOM_38", "
         "ACCEL_26", "ROCR_14", "sd_3", "ACCEL_50", "volsd_3", "ACCEL_44", "ACCEL_56", "ROCR_20",
         "ROCR_56", "PVT", "PSY", "ROCR_32", "MOM_26", "ACCEL_14", "RSI_8", "MOM_50"]
 N_BLOCKS = 8           # fixed asset blocks of the Gram trees (>= the largest GPU count)
-N_CHUNKS = 16          # date chunks of the pooled Gram's row-block partials
+N_CHUNKS = 64          # date chunks of the pooled Gram's row-block partials (2 tree levels)
+CHUNK_TREE = (32, 2)   # the chunks of a row-block: groups of 32, then the 2 results
 
 STAGES = ("factors", "zstats", "xs_gram", "lasso", "predict", "rebalance", "pnl", "fm",
           "analyzer")
 PIPELINE_STAGES = STAGES
+EXCHANGE_STAGES = STAGES + ("exchange",)
 
 
 @dataclass
@@ -120,84 +122,169 @@ def block_assets(lda: int, nblk: int = N_BLOCKS) -> int:
     return max(1, -(-(lda // 64) // nblk)) * 64
 
 
+def _round_up(x: int, m: int = 64) -> int:
+    return (x + m - 1) // m * m
+
+
+def _even(n: int, world: int, rank: int):
+    return n * rank // world, n * (rank + 1) // world
+
+
 class Pipeline:
-    def __init__(self, grid: PanelGrid, cfg: PipelineConfig | None = None):
+    """The chain on one device, or on one rank of ``comm.world`` (``comm``: afm.sharded.Comm).
+
+    Sharding (one process per GPU): rank r owns the asset blocks
+    [8r/N, 8(r+1)/N) of the fixed 8-block split -- its factor panel, z-score statistics, pooled
+    Gram partials (tree over its row-blocks and blocks) and per-date FM partials.  The
+    exchanges: one all-gather of the block results of the pooled Gram (+ the train_end subtree),
+    one all-gather of the test-date predictions and row bits, one all_to_all of per-date FM
+    partials to the date owners (+ an all-gather of the betas), one all-gather of the rebalance
+    results (rebalance dates are split over ranks).  Every sum follows the same fixed trees as
+    one device, so every result is bit-identical to N = 1."""
+
+    def __init__(self, grid: PanelGrid, cfg: PipelineConfig | None = None, comm=None):
         import torch
-        self.g = grid
+        self.full = grid
+        self.comm = comm
+        W = comm.world if comm is not None else 1
+        rk = comm.rank if comm is not None else 0
+        self.W, self.rank = W, rk
         self.cfg = c = cfg or PipelineConfig()
         dev = grid.device
         T, lda, A = grid.T, grid.lda, grid.A
         nch = (T + 63) // 64
-        self.T, self.lda, self.A = T, lda, A
+        self.T, self.lda, self.A, self.nch = T, lda, A, nch
         self.sp = sp = Split.of(grid.dates, c.train_end, c.valid_end)
         self.p = p = len(FEATURES)
         self.p2 = p + 2
+        self.pf = len(c.fm_features)
         f64 = dict(dtype=torch.float64, device=dev)
         i64 = dict(dtype=torch.int64, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
-        self.feat = torch.as_tensor(np.array([COL[n] for n in FEATURES], np.int32), device=dev)
-        self.pf = len(c.fm_features)
-        self.out = torch.full((N_FACTORS, T, lda), float("nan"), **f64)
-        self.nanfree = torch.zeros((nch, lda), **i64)
-        self.finite = torch.zeros((nch, lda), **i64)
-        self.alldf = torch.zeros((nch, lda), **i64)      # all_df rows (NT:33 dropna)
-        self.frows = torch.zeros((nch, lda), **i64)      # all_df rows with every feature finite
-        self.zrows = torch.zeros((nch, lda), **i64)      # rows surviving the z-score dropna
-        self.mu = torch.empty((p, lda), **f64)
-        self.sd = torch.empty((p, lda), **f64)
-        self.zs = torch.empty((p + 1, lda, 2), **f64)
-        self.asset_ok = torch.empty(lda, **i32)
-        self.nblk = N_BLOCKS
-        self.blk = block_assets(lda)
-        self.nrb = (A + 63) // 64                        # 64-asset row-blocks
-        self.rb_per_blk = self.blk // 64
         L = _lib.lib()
-        pe = L.afm_zgram_part_bytes(p) // 8
-        self.pool_part = torch.empty((self.nrb, N_CHUNKS, pe), **f64)
-        self.pool_rb = torch.empty((self.nrb, pe), **f64)
-        self.pool_blk = torch.empty((self.nblk, pe), **f64)
+        # ---- asset shard: whole blocks of the fixed split ----
+        if N_BLOCKS % W:
+            raise ValueError(f"{W} ranks: the GPU count must divide {N_BLOCKS}")
+        self.nblk = N_BLOCKS
+        self.blk = blk = block_assets(lda)
+        self.rb_per_blk = blk // 64
+        self.nblk_r = N_BLOCKS // W
+        self.ranges = []
+        for q in range(W):
+            lo = min(q * self.nblk_r * blk, A)
+            self.ranges.append((lo, min((q + 1) * self.nblk_r * blk, A)))
+        a0, a1 = self.ranges[rk]
+        self.a0, self.A_r = a0, a1 - a0
+        self.lda_r = lda_r = _round_up(max(self.A_r, 1))
+        self.wide = self.nblk_r * blk                  # padded shard width of the exchanges
+        if W == 1:
+            self.g = grid
+        else:
+            sl = slice(a0, a0 + lda_r)
+            self.g = PanelGrid(dates=grid.dates, ids=grid.ids[a0:a1],
+                               close=grid.close[:, sl].contiguous(),
+                               volume=grid.volume[:, sl].contiguous(),
+                               ret1d=grid.ret1d[:, sl].contiguous(),
+                               excess=grid.excess[:, sl].contiguous(),
+                               valid=grid.valid[:, sl].contiguous(),
+                               vbits=grid.vbits[:, sl].contiguous())
+        self.feat = torch.as_tensor(np.array([COL[n] for n in FEATURES], np.int32), device=dev)
+        # ---- local (shard) buffers ----
+        self.out = torch.full((N_FACTORS, T, lda_r), float("nan"), **f64)
+        self.nanfree = torch.zeros((nch, lda_r), **i64)
+        self.finite = torch.zeros((nch, lda_r), **i64)
+        self.alldf = torch.zeros((nch, lda_r), **i64)    # all_df rows (NT:33 dropna)
+        self.frows = torch.zeros((nch, lda_r), **i64)    # all_df rows with every feature finite
+        self.zrows = torch.zeros((nch, lda_r), **i64)    # rows surviving the z-score dropna
+        self.mu = torch.empty((p, lda_r), **f64)
+        self.sd = torch.empty((p, lda_r), **f64)
+        self.zs = torch.empty((p + 1, lda_r, 2), **f64)
+        self.asset_ok = torch.empty(lda_r, **i32)
+        self.nrb = (self.A_r + 63) // 64                 # this shard's 64-asset row-blocks
+        self.pe = pe = L.afm_zgram_part_bytes(p) // 8
+        self.pool_part = torch.empty((max(self.nrb, 1), N_CHUNKS, pe), **f64)
+        self.pool_c1 = torch.empty((max(self.nrb, 1) * (N_CHUNKS // CHUNK_TREE[0]), pe), **f64)
+        self.pool_rb = torch.empty((max(self.nrb, 1), pe), **f64)
+        self.pool_blk = torch.zeros((self.nblk_r + 1, pe), **f64)   # + the train_end subtree
+        self.pool_all = torch.zeros((N_BLOCKS, pe), **f64)
+        self.te_part = torch.zeros((self.nblk_r, pe), **f64)
+        self.te_all = torch.zeros((W, pe), **f64)
         self.pool_g = torch.empty((1, self.p2, self.p2), **f64)
         self.pool_s = torch.zeros((1, self.p2), **f64)   # raw moments: zero shift
-        self.te_part = torch.empty((self.nblk, pe), **f64)
-        self.te_gram = torch.empty((1, self.p2, self.p2), **f64)
+        self.te_gram = torch.zeros((1, self.p2, self.p2), **f64)
         self.lasso_beta = torch.empty(p + 1, **f64)
         self.lasso_info = torch.empty(3, **f64)
-        # FM design: [1, FM30 z-scores, target] per date
+        # FM design: [1, FM30 factor values, target] per date
         self.fm_cols = torch.as_tensor(np.array([COL[n] for n in c.fm_features], np.int32),
                                        device=dev)
-        pef = L.afm_zgram_part_bytes(self.pf) // 8
-        self.fm_part = torch.empty((T, self.nblk, pef), **f64)
-        self.fm_gram = torch.empty((T, self.pf + 2, self.pf + 2), **f64)
-        self.fm_shift = torch.zeros((T, self.pf + 2), **f64)
-        self.pred = torch.full((T, lda), float("nan"), **f64)
-        self.fm_beta = torch.empty((T, self.pf + 1), **f64)
-        self.fm_nobs = torch.empty(T, **f64)
-        self.fm_rank = torch.empty(T, **i32)
+        self.pef = pef = L.afm_zgram_part_bytes(self.pf) // 8
+        self.fm_part = torch.zeros((T, self.nblk_r, pef), **f64)
+        self.fm_sub = torch.zeros((T, pef), **f64)      # this shard's subtree per date
+        self.fdr = [_even(T, W, q) for q in range(W)]   # FM dates owned by each rank
+        fd0, fd1 = self.fdr[rk]
+        self.fd0, self.fnd = fd0, fd1 - fd0
+        self.fnd_max = max(b - a for a, b in self.fdr)
+        self.fm_gram = torch.empty((max(self.fnd, 1), self.pf + 2, self.pf + 2), **f64)
+        self.fm_shift = torch.zeros((max(self.fnd, 1), self.pf + 2), **f64)
+        self.fm_beta_own = torch.full((self.fnd_max, self.pf + 1), float("nan"), **f64)
+        self.fm_nobs_own = torch.zeros(self.fnd_max, **f64)
+        self.fm_rank_own = torch.zeros(self.fnd_max, **i32)
+        if W == 1:
+            self.fm_beta, self.fm_nobs, self.fm_rank = (self.fm_beta_own, self.fm_nobs_own,
+                                                        self.fm_rank_own)
+        else:
+            self.fm_beta = torch.empty((T, self.pf + 1), **f64)
+            self.fm_nobs = torch.empty(T, **f64)
+            self.fm_rank = torch.empty(T, **i32)
         self.fm_mean = torch.empty(self.pf + 1, **f64)
         self.fm_t = torch.empty(self.pf + 1, **f64)
+        self.pred_r = torch.full((T, lda_r), float("nan"), **f64)
+        # ---- full-width planes the rebalance / analyzer read ----
+        if W == 1:
+            self.pred, self.zrows_full, self.alldf_full = self.pred_r, self.zrows, self.alldf
+            self.target, self.tmr = self.out[TARGET], self.out[TMR]
+        else:
+            self.pred = torch.full((T, lda), float("nan"), **f64)
+            self.zrows_full = torch.zeros((nch, lda), **i64)
+            self.alldf_full = torch.zeros((nch, lda), **i64)
+            self.target = torch.full((T, lda), float("nan"), **f64)
+            self.tmr = torch.full((T, lda), float("nan"), **f64)
+            win = c.window if c.window is not None else T
+            self.lab0 = 0 if c.window is None else max(0, sp.s0 - int(win) - 1)
         # rebalance dates: the test dates that can carry predictions (a present observation that
         # is not the asset's last -- every other row lacks the target)
-        vb = grid.valid.cpu().numpy() if hasattr(grid.valid, "cpu") else np.asarray(grid.valid)
+        vb = grid.valid.cpu().numpy()
         nxt = np.zeros_like(vb)
         nxt[:-1] = np.flip(np.logical_or.accumulate(np.flip(vb[1:], 0), 0), 0)
         has = (vb & nxt).any(axis=1)
         rd = np.flatnonzero(has[sp.s0:]).astype(np.int32) + sp.s0
-        self.rdates = torch.from_numpy(rd).to(dev)
         self.nd = nd = len(rd)
-        self.reb = {
-            "k": torch.empty(nd, **i32),
-            "books": torch.full((nd, 2, MAX_BOOK), -1, **i32),
-            "weights": torch.zeros((nd, 2, MAX_BOOK), **f64),
-            "sums": torch.empty((nd, 4), **f64),
-            "upos": torch.empty((nd, 2, 2, MAX_BOOK), **i32),
-            "usize": torch.empty((nd, 2), **i64),
-            "status": torch.empty(nd, **i32),
-        }
+
+        def reb_buffers(n):
+            n = max(n, 1)
+            return {"k": torch.zeros(n, **i32),
+                    "books": torch.full((n, 2, MAX_BOOK), -1, **i32),
+                    "weights": torch.zeros((n, 2, MAX_BOOK), **f64),
+                    "sums": torch.zeros((n, 4), **f64),
+                    "upos": torch.full((n, 2, 2, MAX_BOOK), -1, **i32),
+                    "usize": torch.zeros((n, 2), **i64),
+                    "status": torch.zeros(n, **i32)}
+        self.reb = reb_buffers(nd)
+        # rebalance dates of this rank (+ one neighbour per side: the turnover alignment needs the
+        # adjacent dates' prediction sets)
+        self.rrange = [_even(nd, W, q) for q in range(W)]
+        i0, i1 = self.rrange[rk]
+        self.i0, self.i1 = i0, i1
+        self.e0, self.e1 = (max(i0 - 1, 0), min(i1 + 1, nd)) if W > 1 else (0, nd)
+        self.rd_ext = torch.from_numpy(rd[self.e0:self.e1].copy()).to(dev)
+        self.rdates = torch.from_numpy(rd).to(dev)
+        self.reb_ext = self.reb if W == 1 else reb_buffers(self.e1 - self.e0)
+        self.nr_max = max(b - a for a, b in self.rrange)
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         # analyzer on the test sub-grid (64-date aligned, so the bit words line up)
-        self.a0 = (sp.s0 // 64) * 64
-        Ta = T - self.a0
+        self.an_a0 = (sp.s0 // 64) * 64
+        Ta = T - self.an_a0
         self.Ta = Ta
         self.price_bits = torch.zeros((nch, lda), **i64)  # df_test rows (all_df, date >= valid_end)
         if c.analyzer:
@@ -212,11 +299,11 @@ class Pipeline:
                 "ra": torch.empty((Ta, lda), **i32),
                 "rd": torch.empty((Ta, lda), **i32),
             }
-            ad = np.arange(sp.s0 - self.a0, Ta, dtype=np.int32)    # test dates, sub-grid index
+            ad = np.arange(sp.s0 - self.an_a0, Ta, dtype=np.int32)   # test dates, sub-grid index
             self.an_dates = torch.from_numpy(ad).to(dev)
             self.an_nd = nad = len(ad)
             years = np.asarray(grid.dates).astype("datetime64[Y]").astype(np.int64) + 1970
-            yr = years[self.a0 + ad].astype(np.int32)
+            yr = years[self.an_a0 + ad].astype(np.int32)
             self.an_year0, self.an_nyears = int(yr.min()), int(yr.max() - yr.min() + 1)
             self.an_year = torch.from_numpy(yr).to(dev)
             self.an.update({
@@ -235,55 +322,76 @@ class Pipeline:
         self.main = torch.cuda.Stream(device=dev, priority=-8 if prio else 0)
         self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
+        self.labels_done = torch.cuda.Event()
+
+    def n_asset_days_local(self) -> int:
+        return int(self.g.valid.sum().item())
 
     # ------------------------------------------------------------------------------------------
-    def _pooled_gram(self, h, t0, nt):
-        """Pooled Gram of the rows of the dates [t0, t0 + nt): row-block x chunk partials, then
-        the tree (chunks of a row-block, row-blocks of an asset block, the asset blocks)."""
+    def _pooled_blocks(self, h, t0, nt):
+        """This shard's pooled-Gram block results (rows of the dates [t0, t0 + nt)): row-block x
+        chunk partials, then the tree -- the chunks of a row-block (32, then 2), the row-blocks
+        of an asset block -> pool_blk[0:nblk_r]."""
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
-        T, lda, p = self.T, self.lda, self.p
+        T, lda, p = self.T, self.lda_r, self.p
+        self.pool_blk.zero_()
+        if self.nrb == 0:
+            return
         chk(L.afm_zpool_f64(h, P(self.out), T * lda, lda, P(self.feat), None, p, TARGET,
-                            P(self.zs), p, P(self.zrows), t0, nt, 0, self.nrb, self.A, N_CHUNKS,
-                            P(self.pool_part), 0), "zpool")
-        chk(L.afm_gram_tree_f64(h, p, P(self.pool_part), self.nrb * N_CHUNKS, N_CHUNKS, 0,
-                                P(self.pool_rb)), "tree chunks")
+                            P(self.zs), p, P(self.zrows), t0, nt, 0, self.nrb, self.A_r,
+                            N_CHUNKS, P(self.pool_part), 0), "zpool")
+        c1, c2 = CHUNK_TREE
+        chk(L.afm_gram_tree_f64(h, p, P(self.pool_part), self.nrb * N_CHUNKS, c1, 0,
+                                P(self.pool_c1)), "tree chunks")
+        chk(L.afm_gram_tree_f64(h, p, P(self.pool_c1), self.nrb * c2, c2, 0, P(self.pool_rb)),
+            "tree chunks 2")
         chk(L.afm_gram_tree_f64(h, p, P(self.pool_rb), self.nrb, self.rb_per_blk, 0,
                                 P(self.pool_blk)), "tree row-blocks")
-        nb = -(-self.nrb // self.rb_per_blk)
-        chk(L.afm_gram_tree_f64(h, p, P(self.pool_blk), nb, self.nblk, 1, P(self.pool_g)),
-            "tree blocks")
 
-    def _date_gram(self, h, t, part, gram):
-        """The full Gram of one date (the train_end duplicate)."""
+    def _te_subtree(self, h, t):
+        """This shard's subtree of the train_end date's Gram -> pool_blk[nblk_r]."""
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
-        T, lda, p = self.T, self.lda, self.p
+        T, lda, p = self.T, self.lda_r, self.p
+        if self.nrb == 0:
+            return
         chk(L.afm_zgram_f64(h, P(self.out), T * lda, lda, P(self.feat), None, p, TARGET,
-                            P(self.zs), p, P(self.zrows), t, 1, self.nblk, 0, self.blk, self.A,
-                            P(part), 0), "zgram date")
-        chk(L.afm_gram_tree_f64(h, p, P(part), self.nblk, self.nblk, 1, P(gram)), "tree date")
+                            P(self.zs), p, P(self.zrows), t, 1, self.nblk_r, 0, self.blk,
+                            self.A_r, P(self.te_part), 0), "zgram date")
+        chk(L.afm_gram_tree_f64(h, p, P(self.te_part), self.nblk_r, self.nblk_r, 0,
+                                P(self.pool_blk[self.nblk_r:])), "tree date")
 
-    def _fm(self, h):
-        """Per-date FM30 Grams, solves and Fama-MacBeth statistics."""
+    def _fm_local(self, h):
+        """This shard's per-date FM30 partials, merged over its blocks -> fm_sub [T]."""
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
-        T, lda, p, pf, c = self.T, self.lda, self.p, self.pf, self.cfg
+        T, lda, pf = self.T, self.lda_r, self.pf
+        if self.nrb == 0:
+            return
         chk(L.afm_zgram_f64(h, P(self.out), T * lda, lda, P(self.fm_cols), None, pf, TARGET,
-                            None, 0, P(self.zrows), 0, T, self.nblk, 0, self.blk, self.A,
+                            None, 0, P(self.zrows), 0, T, self.nblk_r, 0, self.blk, self.A_r,
                             P(self.fm_part), 0), "zgram fm")
-        chk(L.afm_gram_tree_f64(h, pf, P(self.fm_part), T * self.nblk, self.nblk, 1,
-                                P(self.fm_gram)), "tree fm")
-        chk(L.afm_ols_solve_f64(h, P(self.fm_gram), P(self.fm_shift), pf, T, c.tol,
-                                P(self.fm_beta), P(self.fm_nobs), P(self.fm_rank)), "fm solve")
-        chk(L.afm_fama_macbeth_f64(h, P(self.fm_beta), P(self.fm_rank), T, pf + 1,
-                                   P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
+        chk(L.afm_gram_tree_f64(h, pf, P(self.fm_part), T * self.nblk_r, self.nblk_r, 0,
+                                P(self.fm_sub)), "tree fm blocks")
+
+    def _fm_solve(self, h, sub):
+        """Owned dates: the rank subtrees ``sub`` [fnd][W][part] -> Grams, solves; every rank then
+        gets every date's betas and the FM statistics."""
+        L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+        c, pf, T = self.cfg, self.pf, self.T
+        if self.fnd > 0:
+            chk(L.afm_gram_tree_f64(h, pf, P(sub), self.fnd * self.W, self.W, 1,
+                                    P(self.fm_gram)), "tree fm ranks")
+            chk(L.afm_ols_solve_f64(h, P(self.fm_gram), P(self.fm_shift), pf, self.fnd, c.tol,
+                                    P(self.fm_beta_own), P(self.fm_nobs_own),
+                                    P(self.fm_rank_own)), "fm solve")
 
     def step(self, events: dict | None = None):
         """One pass of the chain.  ``events``: optional {stage: (start, end)} CUDA events."""
         import torch
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
-        g, c, sp = self.g, self.cfg, self.sp
-        T, lda, p = self.T, self.lda, self.p
-        nch = (T + 63) // 64
-        caller = torch.cuda.current_stream(g.device)
+        g, c, sp, cm = self.g, self.cfg, self.sp, self.comm
+        T, lda_r, p, W, nch = self.T, self.lda_r, self.p, self.W, self.nch
+        full = self.full
+        caller = torch.cuda.current_stream(full.device)
         for s in (self.main, self.side, self.side2):
             s.wait_stream(caller)
 
@@ -294,47 +402,81 @@ class Pipeline:
         with torch.cuda.stream(self.main):
             h = self.ctx.bind_stream()
             mark("factors", 0)
-            chk(L.afm_factors_f64(h, T, g.A, lda, P(g.close), P(g.volume), P(g.ret1d),
-                                  P(g.excess), P(g.vbits), P(self.out), P(self.nanfree),
-                                  P(self.finite)), "factors")
-            chk(L.afm_drop_last_obs_bits(h, T, lda, P(g.vbits), P(self.nanfree), P(self.alldf)),
-                "all_df rows")
-            chk(L.afm_drop_last_obs_bits(h, T, lda, P(g.vbits), P(self.finite), P(self.frows)),
-                "finite rows")
+            if self.A_r > 0:
+                chk(L.afm_factors_f64(h, T, self.A_r, lda_r, P(g.close), P(g.volume),
+                                      P(g.ret1d), P(g.excess), P(g.vbits), P(self.out),
+                                      P(self.nanfree), P(self.finite)), "factors")
+                chk(L.afm_drop_last_obs_bits(h, T, lda_r, P(g.vbits), P(self.nanfree),
+                                             P(self.alldf)), "all_df rows")
+                chk(L.afm_drop_last_obs_bits(h, T, lda_r, P(g.vbits), P(self.finite),
+                                             P(self.frows)), "finite rows")
             mark("factors", 1)
             mark("zstats", 0)
-            chk(L.afm_zscore_stats_f64(h, P(self.out), T * lda, T, lda, P(self.feat), p,
-                                       P(self.alldf), 0, sp.tr1, P(self.mu), P(self.sd)),
-                "zscore stats")
-            chk(L.afm_zstats_finalize_f64(h, P(self.mu), P(self.sd), p, lda, P(self.zs),
-                                          P(self.asset_ok)), "zstats finalize")
-            chk(L.afm_row_bits(h, nch, lda, P(self.frows), None, P(self.asset_ok), 0, T,
-                               P(self.zrows)), "z rows")
+            if self.A_r > 0:
+                chk(L.afm_zscore_stats_f64(h, P(self.out), T * lda_r, T, lda_r, P(self.feat), p,
+                                           P(self.alldf), 0, sp.tr1, P(self.mu), P(self.sd)),
+                    "zscore stats")
+                chk(L.afm_zstats_finalize_f64(h, P(self.mu), P(self.sd), p, lda_r, P(self.zs),
+                                              P(self.asset_ok)), "zstats finalize")
+                chk(L.afm_row_bits(h, nch, lda_r, P(self.frows), None, P(self.asset_ok), 0, T,
+                                   P(self.zrows)), "z rows")
             mark("zstats", 1)
-            # side stream: the per-date FM30 regressions (nothing downstream reads them)
+            if W > 1:           # full-width label planes for the rebalance, during the Grams
+                with torch.cuda.stream(self.side2):
+                    h2 = self.ctx.bind_stream()
+                    chk(L.afm_labels_f64(h2, T, full.lda, self.lab0, T, P(full.excess),
+                                         P(full.ret1d), P(full.vbits), P(self.target),
+                                         P(self.tmr)), "labels")
+                    self.labels_done.record(self.side2)
+                h = self.ctx.bind_stream()
+            mark("xs_gram", 0)
+            self._pooled_blocks(h, 0, sp.v1)                        # train + valid rows
+            if sp.dup:                                              # train_end counted twice
+                self._te_subtree(h, sp.tr1 - 1)
+            if W > 1:
+                mark("exchange", 0)
+                gb = cm.all_gather(self.pool_blk)                   # [W][nblk_r + 1][part]
+                self.pool_all.copy_(gb[:, :self.nblk_r].reshape(N_BLOCKS, self.pe))
+                self.te_all.copy_(gb[:, self.nblk_r])
+                mark("exchange", 1)
+                h = self.ctx.bind_stream()
+                blocks, te_leaves, nte = self.pool_all, self.te_all, W
+            else:
+                blocks, te_leaves, nte = self.pool_blk, self.pool_blk[self.nblk_r:], 1
+            chk(L.afm_gram_tree_f64(h, p, P(blocks), N_BLOCKS, N_BLOCKS, 1, P(self.pool_g)),
+                "tree blocks")
+            if sp.dup:
+                chk(L.afm_gram_tree_f64(h, p, P(te_leaves), nte, nte, 1, P(self.te_gram)),
+                    "tree train_end")
+                chk(L.afm_vec_add_f64(h, self.p2 * self.p2, P(self.te_gram), P(self.pool_g)),
+                    "dup")
+            mark("xs_gram", 1)
+            # side stream: this shard's per-date FM30 partials (nothing downstream reads them),
+            # forked after the pooled Gram -- run beside it, both MFMA kernels slow down (A/B on
+            # MI355X: pooled Gram 12.7 ms alone, 23 ms beside the FM Grams)
             self.side.wait_stream(self.main)
             with torch.cuda.stream(self.side):
                 hs = self.ctx.bind_stream()
                 mark("fm", 0)
-                self._fm(hs)
+                self._fm_local(hs)
+                if W == 1:
+                    self._fm_solve(hs, self.fm_sub)
+                    self._fm_stats(hs)
                 mark("fm", 1)
             h = self.ctx.bind_stream()
-            mark("xs_gram", 0)
-            self._pooled_gram(h, 0, sp.v1)                          # train + valid rows
-            if sp.dup:                                              # train_end counted twice
-                self._date_gram(h, sp.tr1 - 1, self.te_part, self.te_gram)
-                chk(L.afm_vec_add_f64(h, self.p2 * self.p2, P(self.te_gram), P(self.pool_g)),
-                    "dup")
-            mark("xs_gram", 1)
             mark("lasso", 0)
             chk(L.afm_lasso_fit_f64(h, P(self.pool_g), P(self.pool_s), p, c.alpha, c.max_iter,
                                     c.lasso_tol, 0, P(self.lasso_beta), P(self.lasso_info)),
                 "lasso")
             mark("lasso", 1)
             mark("predict", 0)
-            chk(L.afm_zpredict_f64(h, P(self.out), T * lda, lda, sp.s0, T - sp.s0, P(self.feat),
-                                   p, P(self.zs), P(self.lasso_beta), P(self.zrows),
-                                   P(self.pred)), "predict")
+            if self.A_r > 0:
+                chk(L.afm_zpredict_f64(h, P(self.out), T * lda_r, lda_r, sp.s0, T - sp.s0,
+                                       P(self.feat), p, P(self.zs), P(self.lasso_beta),
+                                       P(self.zrows), P(self.pred_r)), "predict")
+            if W > 1:                          # the whole cross-section of the test dates
+                self._gather_test_planes()
+                h = self.ctx.bind_stream()
             mark("predict", 1)
             if c.analyzer:
                 self.side2.wait_stream(self.main)
@@ -342,39 +484,114 @@ class Pipeline:
                     self._analyzer(mark)
                 h = self.ctx.bind_stream()
             mark("rebalance", 0)
-            r = self.reb
-            chk(L.afm_rebalance_f64(h, T, g.A, lda, P(self.rdates), self.nd, P(self.pred),
-                                    P(g.tbits), P(self.out[TARGET]), P(self.zrows), 0, sp.tr1,
-                                    -1 if c.window is None else int(c.window), P(g.close),
-                                    P(self.out[TMR]), c.top_n, c.lo, c.hi, P(r["k"]),
-                                    P(r["books"]), P(r["weights"]), P(r["sums"]), P(r["upos"]),
-                                    P(r["usize"]), P(r["status"])), "rebalance")
+            if W > 1:
+                self.main.wait_event(self.labels_done)     # the label planes
+            x = self.reb_ext
+            ne = self.e1 - self.e0
+            if ne > 0:
+                chk(L.afm_rebalance_f64(h, T, full.A, full.lda, P(self.rd_ext), ne, P(self.pred),
+                                        P(full.tbits), P(self.target), P(self.zrows_full), 0,
+                                        sp.tr1, -1 if c.window is None else int(c.window),
+                                        P(full.close), P(self.tmr), c.top_n, c.lo, c.hi,
+                                        P(x["k"]), P(x["books"]), P(x["weights"]), P(x["sums"]),
+                                        P(x["upos"]), P(x["usize"]), P(x["status"])), "rebalance")
+            if W > 1:
+                self._gather_rebalance()
+                h = self.ctx.bind_stream()
             mark("rebalance", 1)
             mark("pnl", 0)
-            q = self.pnl
+            r, q = self.reb, self.pnl
             chk(L.afm_pnl_scan_f64(h, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]),
                                    P(r["upos"]), P(r["usize"]), c.v0, c.rate, P(q["value"]),
                                    P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])), "pnl")
             mark("pnl", 1)
+            if W > 1:          # FM: per-date subtrees -> date owners (issued after the main chain)
+                self.main.wait_stream(self.side)
+                self._fm_exchange()
         for s in (self.main, self.side, self.side2):
             caller.wait_stream(s)
         self.ctx.bind_stream()
 
+    # ---- exchanges (N > 1) -------------------------------------------------------------------
+    def _place(self, dst, gathered, rows=None):
+        """Scatter per-rank shard columns ([W][rows][wide]) into a full-width plane."""
+        for q, (lo, hi) in enumerate(self.ranges):
+            if hi > lo:
+                if rows is None:
+                    dst[:, lo:hi] = gathered[q][:, :hi - lo]
+                else:
+                    dst[rows, lo:hi] = gathered[q][:, :hi - lo]
+
+    def _gather_test_planes(self):
+        import torch
+        s0, wide, A_r = self.sp.s0, self.wide, self.A_r
+        pr = torch.full((self.T - s0, wide), float("nan"), dtype=torch.float64,
+                        device=self.pred_r.device)
+        zb = torch.zeros((self.nch, wide), dtype=torch.int64, device=self.pred_r.device)
+        ab = torch.zeros_like(zb)
+        if A_r > 0:
+            pr[:, :A_r] = self.pred_r[s0:, :A_r]
+            zb[:, :A_r] = self.zrows[:, :A_r]
+            ab[:, :A_r] = self.alldf[:, :A_r]
+        gp, gz, ga = self.comm.all_gather_packed([pr, zb, ab])
+        self._place(self.pred, gp, rows=slice(s0, self.T))
+        self._place(self.zrows_full, gz)
+        self._place(self.alldf_full, ga)
+
+    def _gather_rebalance(self):
+        import torch
+        x = self.reb_ext
+        lo = self.i0 - self.e0
+        n_own = self.i1 - self.i0
+        owns = []
+        for k, v in x.items():
+            own = v[lo:lo + n_own]
+            if n_own < self.nr_max:
+                pad = torch.zeros((self.nr_max - n_own,) + tuple(v.shape[1:]), dtype=v.dtype,
+                                  device=v.device)
+                own = torch.cat([own, pad])
+            owns.append(own)
+        for k, gath in zip(x.keys(), self.comm.all_gather_packed(owns)):
+            for q, (qlo, qhi) in enumerate(self.rrange):
+                self.reb[k][qlo:qhi] = gath[q, :qhi - qlo]
+
+    def _fm_exchange(self):
+        import torch
+        W, pef = self.W, self.pef
+        splits = [b - a for a, b in self.fdr]
+        recv = self.comm.all_to_all(self.fm_sub, splits, [self.fnd] * W)   # [W * fnd][part]
+        sub = recv.view(W, self.fnd, pef).transpose(0, 1).contiguous()     # [fnd][W][part]
+        h = self.ctx.bind_stream()
+        self._fm_solve(h, sub)
+        bg, ng, kg = self.comm.all_gather_packed([self.fm_beta_own, self.fm_nobs_own,
+                                                  self.fm_rank_own])
+        for q, (lo, hi) in enumerate(self.fdr):
+            self.fm_beta[lo:hi] = bg[q, :hi - lo]
+            self.fm_nobs[lo:hi] = ng[q, :hi - lo]
+            self.fm_rank[lo:hi] = kg[q, :hi - lo]
+        self._fm_stats(self.ctx.bind_stream())
+
+    def _fm_stats(self, h):
+        L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+        chk(L.afm_fama_macbeth_f64(h, P(self.fm_beta), P(self.fm_rank), self.T, self.pf + 1,
+                                   P(self.fm_mean), P(self.fm_t)), "fama_macbeth")
+
+    # ------------------------------------------------------------------------------------------
     def _analyzer(self, mark):
         """AlphaSignalAnalyzer(lasso_predict, price_data=df_test[['close_price']]).run()
         (KKT:630-631) on the test sub-grid, no host synchronisation."""
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
-        g, sp, an = self.g, self.sp, self.an
-        T, lda, a0, Ta = self.T, self.lda, self.a0, self.Ta
-        nch = (T + 63) // 64
+        full, sp, an = self.full, self.sp, self.an
+        T, lda, a0, Ta = self.T, full.lda, self.an_a0, self.Ta
+        nch = self.nch
         h = self.ctx.bind_stream()
         mark("analyzer", 0)
-        chk(L.afm_row_bits(h, nch, lda, P(self.alldf), None, None, sp.s0, T, P(self.price_bits)),
-            "price rows")
+        chk(L.afm_row_bits(h, nch, lda, P(self.alldf_full), None, None, sp.s0, T,
+                           P(self.price_bits)), "price rows")
         cb = a0 // 64
-        chk(L.afm_fwd_returns_f64(h, Ta, lda, P(g.close[a0:]), P(self.price_bits[cb:]),
+        chk(L.afm_fwd_returns_f64(h, Ta, lda, P(full.close[a0:]), P(self.price_bits[cb:]),
                                   P(an["fr"])), "fwd_returns")
-        chk(L.afm_xs_prepare_f64(h, Ta, g.A, lda, P(self.pred[a0:]), P(an["fr"]),
+        chk(L.afm_xs_prepare_f64(h, Ta, full.A, lda, P(self.pred[a0:]), P(an["fr"]),
                                  P(an["scratch"]), P(an["rows"]), P(an["rows_idx"]),
                                  P(an["nrows"])), "xs_prepare")
         chk(L.afm_xs_rank_f64(h, Ta, lda, P(an["rows"]), P(an["nrows"]), P(an["skey"]),

@@ -97,7 +97,7 @@ def test_analyzer_series_vs_golden(chain_a):
     p, pipe, gold, C = chain_a
     an = pipe.an
     ic = an["ic"].cpu().numpy()
-    d = pipe.an_dates.cpu().numpy() + pipe.a0
+    d = pipe.an_dates.cpu().numpy() + pipe.an_a0
     dint = p.dates.astype("datetime64[ns]").astype(np.int64)
     types = {"return_1": 0, "return_2": 1, "return_5": 2}
     pos = {x: i for i, x in enumerate(dint[d].tolist())}

@@ -1,10 +1,10 @@
-"""Multi-rank path (afm/sharded.py).
+"""Multi-rank path (afm/pipeline.py with a Comm).
 
-CPU (gloo, world size 2): shard ranges and the Comm collectives the step uses (equal-shape
-all-gather, all_to_all with uneven splits), plus the per-date moment merge algebra the date owner
-applies to the per-rank partial Grams.  GPU: two ranks sharing cuda:0 over gloo run the full
-sharded step and match the single-process Pipeline (betas / pooled OLS rel 1e-9, books exact,
-PnL rel 1e-12).
+CPU (gloo, world size 2 and 4): shard geometry, the Comm collectives the step uses (equal-shape
+all-gather, all_to_all with uneven splits, packed all-gather), and the subtree exchange: a rank's
+subtree sum, all-gathered and summed over the same tree, equals the one-process tree bit for bit.
+GPU: 2 and 4 ranks sharing cuda:0 over gloo run the whole step and are BIT-identical to the
+single-device Pipeline (pooled Gram, Lasso, predictions, FM betas, books, weights, PnL, IC).
 """
 import os
 import socket
@@ -85,49 +85,59 @@ def test_comm_gloo_collectives(tmp_path):
     assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
 
 
-def _shifted_moments(Z):
-    """The Gram kernel's representation of rows Z [n][p+1] (x.., y): G'[0][0] = n,
-    G'[0][j] = sum(z_j - s_j), G'[i][j] = sum (z_i - s_i)(z_j - s_j), s = first row."""
-    n = len(Z)
-    s = Z[0].copy()
-    D = np.column_stack([np.ones(n), Z - s])
-    return D.T @ D, np.r_[0.0, s]
+def tree_sum(v):
+    """afm_gram_tree_f64's tree over the leaves v[0..n) (strides 1, 2, 4, ...)."""
+    v = [x.copy() for x in v]
+    n = len(v)
+    s = 1
+    while s < n:
+        for i in range(0, n - s, 2 * s):
+            v[i] = v[i] + v[i + s]
+        s *= 2
+    return v[0]
 
 
-def _merge(parts):
-    """pool_kernel's combination (Chan), in order, -> (n, mean, centered cross moments)."""
-    ntot, mu, C = 0.0, None, None
-    for G, s in parts:
-        nb = G[0, 0]
-        if not nb > 0:
-            continue
-        cb = G[1:, 1:] - np.outer(G[0, 1:], G[0, 1:]) / nb
-        mb = s[1:] + G[0, 1:] / nb
-        if C is None:
-            C, mu, ntot = cb.copy(), mb.copy(), nb
-            continue
-        dl = mb - mu
-        fac = ntot * nb / (ntot + nb)
-        C = C + cb + np.outer(dl, dl) * fac
-        ntot = ntot + nb
-        mu = mu + dl * (nb / ntot)
-    return ntot, mu, C
+def _tree_worker(rank, world, port, outdir):
+    """Each rank sums its aligned run of the 8 block leaves (its subtree), the results are
+    all-gathered and summed over the same tree: bit-identical to the one-process sum."""
+    import torch
+    _init(rank, world, port)
+    from afm.sharded import Comm
+    cm = Comm()
+    rng = np.random.default_rng(5)
+    leaves = [rng.normal(0, 1, 257) * 10.0 ** rng.integers(-8, 8) for _ in range(8)]
+    per = 8 // world
+    mine = tree_sum(leaves[rank * per:(rank + 1) * per])
+    g = cm.all_gather(torch.from_numpy(mine))
+    total = tree_sum([g[q].numpy() for q in range(world)])
+    assert np.array_equal(total, tree_sum(leaves))
+    cm.barrier()
+    open(os.path.join(outdir, f"tree{rank}"), "w").write("ok")
 
 
-def test_partial_moment_merge_equals_full_date():
-    """The owner of a date merges the per-rank partials of its asset shards: the result equals
-    the centered moments of the whole cross-section (the algebra of afm_pool_segments_f64)."""
-    rng = np.random.default_rng(3)
-    Z = rng.normal(50, 3, (1000, 8))
-    Z[:, -1] = Z[:, :3].sum(axis=1) * 0.01 + rng.normal(0, 1e-3, 1000)
-    cuts = [0, 128, 128, 640, 1000]                     # includes an empty shard
-    parts = [_shifted_moments(Z[a:b]) if b > a else (np.zeros((9, 9)), np.zeros(9))
-             for a, b in zip(cuts, cuts[1:])]
-    n, mu, C = _merge(parts)
-    assert n == 1000
-    assert np.allclose(mu, Z.mean(axis=0), rtol=1e-13)
-    ref = (Z - Z.mean(axis=0)).T @ (Z - Z.mean(axis=0))
-    assert np.abs(C - ref).max() <= 1e-11 * np.abs(ref).max()
+@pytest.mark.parametrize("world", [2, 4])
+def test_subtree_exchange_is_bit_identical(tmp_path, world):
+    import torch.multiprocessing as mp
+    port = _free_port()
+    mp.spawn(_tree_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / f"tree{q}").exists() for q in range(world))
+
+
+def test_shard_geometry():
+    """Ranks own whole blocks of the fixed 8-block split (64-aligned, covering every asset)."""
+    from afm.pipeline import N_BLOCKS, block_assets
+    for A in (44, 300, 500, 1000, 10000):
+        lda = (A + 63) // 64 * 64
+        blk = block_assets(lda)
+        assert blk % 64 == 0 and blk * N_BLOCKS >= A
+        for W in (1, 2, 4, 8):
+            per = N_BLOCKS // W
+            rs = [(min(q * per * blk, A), min((q + 1) * per * blk, A)) for q in range(W)]
+            assert rs[0][0] == 0 and rs[-1][1] == A
+            assert all(b == c for (_, b), (c, _) in zip(rs, rs[1:]))
+
+
+SPLIT = dict(train_end="2001-06-29", valid_end="2001-12-31", window=120)
 
 
 def _sharded_worker(rank, world, port, outdir, A, T):
@@ -139,53 +149,51 @@ def _sharded_worker(rank, world, port, outdir, A, T):
     from afm.synthetic import make_panel
     torch.cuda.set_device(0)
     grid = afm.PanelGrid.from_panel(make_panel(A, T, seed=11, tradable_p=0.9))
-    cfg = PipelineConfig(cols=[afm.FACTOR_NAMES.index(c) for c in WELL], window=120)
-    sp = ShardedPipeline(grid, Comm(), cfg)
+    sp = ShardedPipeline(grid, Comm(), PipelineConfig(**SPLIT))
     sp.step()
     sp.step()
     torch.cuda.synchronize()
     if rank == 0:
-        np.savez(os.path.join(outdir, "sharded.npz"), beta=sp.beta.cpu().numpy(),
-                 nobs=sp.nobs.cpu().numpy(), pool=sp.pool_beta.cpu().numpy(),
-                 fm=sp.fm_mean.cpu().numpy(), k=sp.reb["k"].cpu().numpy(),
-                 books=sp.reb["books"].cpu().numpy(), value=sp.pnl["value"].cpu().numpy(),
-                 pred=sp.pred.cpu().numpy())
+        np.savez(os.path.join(outdir, "sharded.npz"), pool=sp.pool_g.cpu().numpy(),
+                 beta=sp.lasso_beta.cpu().numpy(), pred=sp.pred.cpu().numpy(),
+                 fm=sp.fm_beta.cpu().numpy(), fm_mean=sp.fm_mean.cpu().numpy(),
+                 k=sp.reb["k"].cpu().numpy(), books=sp.reb["books"].cpu().numpy(),
+                 w=sp.reb["weights"].cpu().numpy(), value=sp.pnl["value"].cpu().numpy(),
+                 ic=sp.an["ic"].cpu().numpy())
     Comm().barrier()
 
 
-WELL = ["RSI_14", "sd_5", "corr_15", "PSY", "ROCR_20", "volsd5_15", "MACD_12_24"]
-
-
 @pytest.mark.gpu
-def test_sharded_two_ranks_match_single(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_ranks_bit_identical_to_single(tmp_path, world):
+    """N ranks (gloo, sharing cuda:0) run the whole step: the pooled Gram, Lasso, predictions,
+    FM betas, books, weights, PnL and IC are BIT-identical to the one-device step."""
     import torch
     import torch.multiprocessing as mp
     import afm
     from afm.pipeline import Pipeline, PipelineConfig
     from afm.synthetic import make_panel
-    A, T = 300, 700                              # 5 asset blocks, 11 date blocks: uneven shards
+    A, T = 300, 700                              # 5 asset groups: blocks of 64, ranks uneven
     port = _free_port()
-    mp.spawn(_sharded_worker, args=(2, port, str(tmp_path), A, T), nprocs=2, join=True)
+    mp.spawn(_sharded_worker, args=(world, port, str(tmp_path), A, T), nprocs=world, join=True)
     s = np.load(tmp_path / "sharded.npz")
     grid = afm.PanelGrid.from_panel(make_panel(A, T, seed=11, tradable_p=0.9))
-    cfg = PipelineConfig(cols=[afm.FACTOR_NAMES.index(c) for c in WELL], window=120)
-    pipe = Pipeline(grid, cfg)
+    pipe = Pipeline(grid, PipelineConfig(**SPLIT))
     pipe.step()
     torch.cuda.synchronize()
-    b1 = pipe.beta.cpu().numpy()
-    ok = pipe.nobs.cpu().numpy() > len(WELL) + 5
-    assert np.array_equal(s["nobs"], pipe.nobs.cpu().numpy())
-    err = np.abs(s["beta"][ok] - b1[ok]).max(axis=1) / np.abs(b1[ok]).max(axis=1)
-    assert err.max() < 1e-9, err.max()
-    pb = pipe.pool_beta.cpu().numpy()
-    assert np.abs(s["pool"] - pb).max() / np.abs(pb).max() < 1e-9
-    fm = pipe.fm_mean.cpu().numpy()
-    assert np.abs(s["fm"] - fm).max() / np.abs(fm).max() < 1e-9
+    assert np.array_equal(s["pool"], pipe.pool_g.cpu().numpy())
+    assert np.array_equal(s["beta"], pipe.lasso_beta.cpu().numpy())
     pr = pipe.pred.cpu().numpy()
-    both = ~np.isnan(pr)
-    assert np.array_equal(both, ~np.isnan(s["pred"]))
-    assert np.abs(s["pred"][both] - pr[both]).max() / np.abs(pr[both]).max() < 1e-9
+    assert np.array_equal(np.isnan(s["pred"]), np.isnan(pr))
+    assert np.array_equal(s["pred"][~np.isnan(pr)], pr[~np.isnan(pr)])
+    fm = pipe.fm_beta.cpu().numpy()
+    assert np.array_equal(np.isnan(s["fm"]), np.isnan(fm))
+    assert np.array_equal(s["fm"][~np.isnan(fm)], fm[~np.isnan(fm)])
+    assert np.array_equal(s["fm_mean"], pipe.fm_mean.cpu().numpy())
     assert np.array_equal(s["k"], pipe.reb["k"].cpu().numpy())
     assert np.array_equal(s["books"], pipe.reb["books"].cpu().numpy())
-    v = pipe.pnl["value"].cpu().numpy()
-    assert np.abs(s["value"] - v).max() / v.max() < 1e-12
+    assert np.array_equal(s["w"], pipe.reb["weights"].cpu().numpy())
+    assert np.array_equal(s["value"], pipe.pnl["value"].cpu().numpy())
+    ic = pipe.an["ic"].cpu().numpy()
+    assert np.array_equal(np.isnan(s["ic"]), np.isnan(ic))
+    assert np.array_equal(s["ic"][~np.isnan(ic)], ic[~np.isnan(ic)])

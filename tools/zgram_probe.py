@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--grid", type=int, default=0)
     ap.add_argument("--check", type=int, default=1)
+    ap.add_argument("--chunks", type=str, default="16,32,64")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -37,16 +38,29 @@ def main():
     v1 = pipe.sp.v1
     h = pipe.ctx.bind_stream()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    for nc in [int(x) for x in a.chunks.split(",")]:
+        part = torch.empty((pipe.nrb, nc, pipe.pe), dtype=torch.float64, device=pipe.out.device)
+        ts = []
+        for _ in range(a.reps):
+            ev[0].record()
+            _lib.check(L.afm_zpool_f64(h, P(pipe.out), T * lda, lda, P(pipe.feat), None, pipe.p,
+                                       96, P(pipe.zs), pipe.p, P(pipe.zrows), 0, v1, 0, pipe.nrb,
+                                       pipe.A, nc, P(part), a.grid), "zpool")
+            ev[1].record()
+            torch.cuda.synchronize()
+            ts.append(ev[0].elapsed_time(ev[1]))
+        print(f"zpool with {nc} chunks: {np.median(ts):.3f} ms (min {min(ts):.3f})", flush=True)
+        del part
     tz, tm, tf = [], [], []
     for _ in range(a.reps):
         ev[0].record()
         _lib.check(L.afm_zpool_f64(h, P(pipe.out), T * lda, lda, P(pipe.feat), None, pipe.p, 96,
                                    P(pipe.zs), pipe.p, P(pipe.zrows), 0, v1, 0, pipe.nrb, pipe.A,
-                                   16, P(pipe.pool_part), a.grid), "zpool")
+                                   64, P(pipe.pool_part), a.grid), "zpool")
         ev[1].record()
-        pipe._pooled_gram(h, 0, v1)
+        pipe._pooled_blocks(h, 0, v1)
         ev[2].record()
-        pipe._fm(h)
+        pipe._fm_local(h)
         ev[3].record()
         torch.cuda.synchronize()
         tz.append(ev[0].elapsed_time(ev[1]))
@@ -69,6 +83,9 @@ def main():
         y = pipe.out[96][tt, aa]
         D = torch.cat([torch.ones_like(y)[:, None], Z, y[:, None]], dim=1)
         G = D.T @ D
+        if pipe.sp.dup:                                   # train_end's rows count twice
+            te = tt == pipe.sp.tr1 - 1
+            G = G + D[te].T @ D[te]
         err = ((pipe.pool_g[0] - G).abs().max() / G.abs().max()).item()
         print(f"pooled gram vs torch fp64 reference: rel err {err:.3g}", flush=True)
         worst = 0.0
