@@ -366,6 +366,8 @@ constexpr int kStatRows = 512;
 __global__ __launch_bounds__(128) void xs_stats_kernel(StatArgs g) {
     __shared__ double sv[4][kStatRows];          // factor, return_1, return_2, return_5
     __shared__ int8_t slay[kStatRows];
+    __shared__ double sinv[kStatRows];           // 1 / (row number): the Welford divisor when no
+                                                 // row has been skipped (IEEE, as 1. / nobs)
     __shared__ double pv_f[kTopK], pv_r[3][kTopK];
     __shared__ int pv_has[kTopK];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -388,6 +390,7 @@ __global__ __launch_bounds__(128) void xs_stats_kernel(StatArgs g) {
         for (int e = tid; e < len; e += 128) {
             const int64_t o = base + c0 + e;
             sv[0][e] = g.rows[o];
+            sinv[e] = 1. / (double)(c0 + e + 1);
             for (int q = 0; q < 3; ++q) sv[1 + q][e] = g.rows[(1 + q) * plane + o];
             const double pct = (double)g.rank_asc[o] / (double)n;     // KKT:328-330
             int layer = (int)(pct * kLayers) + 1;
@@ -408,8 +411,10 @@ __global__ __launch_bounds__(128) void xs_stats_kernel(StatArgs g) {
                 if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
                     nobs += 1;
                     const double dx = vx - mx, dy = vy - my;
-                    mx += 1. / nobs * dx;
-                    my += 1. / nobs * dy;
+                    // the same value as 1. / nobs, off the dependency chain while no row is skipped
+                    const double inv = nobs == (double)(c0 + e + 1) ? sinv[e] : 1. / nobs;
+                    mx += inv * dx;
+                    my += inv * dy;
                     sxx += (vx - mx) * dx;
                     syy += (vy - my) * dy;
                     sxy += (vx - mx) * dy;

@@ -6,8 +6,8 @@ Workload (N=1): BASELINE.json configs[2] -- 10,000 assets x 20 years (5,040 trad
 synthetic panel (seeded generator, SURVEY.md §8(d): ragged listings, 0.2% holes, 90% tradable),
 inputs resident in HBM before the timed region.  One step = afm.pipeline.Pipeline.step(), the
 reference chain that feeds PortfolioManager: 98-column factor build (NT:1-93) -> train-window
-per-security z-score of the 97 features (KKT:424-458, the reference's split dates) -> per-date
-Grams of [1, z_1..z_97, target] on fp64 MFMA -> pooled train+valid moments + Lasso(alpha=2e-4)
+per-security z-score of the 97 features (KKT:424-458, the reference's split dates) -> pooled
+train+valid Gram of [1, z_1..z_97, target] on fp64 MFMA (z applied on the fly) -> Lasso(alpha=2e-4)
 (KKT:605-607) -> test predictions (KKT:612) -> rolling-252-day covariance + exact min-variance
 KKT weights for top/bottom-10 books on every test date + PnL/turnover scan (KKT:976-977); side
 streams: AlphaSignalAnalyzer on the predictions (KKT:630-631) and the per-date FM30 OLS +
@@ -60,11 +60,34 @@ def pmc_traffic(stage: str, assets: int, days: int):
     return sum(ks[k]["hbm_bytes"] for k in ROOF_KERNELS[stage])
 
 
-def cpu_baseline(seed: int, assets: int = 150, days: int = 2520):
-    """The oracle chain (oracle/chain.py: C factor restatement, numpy z-score, scikit-learn Lasso,
-    exact-QP PortfolioManager, analyzer, per-date FM lstsq), 1 core, on a bounded sample of
-    config A's calendar (``assets`` x 2,520 days; the reference's own split rule)."""
-    import numpy as np
+def cpu_baseline(seed: int, assets: int = 100, days: int = 2520):
+    """The reference's CPU path in its own call pattern (oracle/pandas_chain.py: per-security
+    pandas factor loop, groupby z-score, scikit-learn Lasso, pandas analyzer, per-date all_df
+    filter + SLSQP PortfolioManager loop), 1 core, on a bounded sample of config A's calendar
+    (``assets`` x 2,520 days, the reference's split rule).  The value path it produces equals
+    oracle/chain.py's bit for bit (tests/test_pandas_chain.py)."""
+    from threadpoolctl import threadpool_limits
+
+    from afm.synthetic import make_panel
+    from oracle import pandas_chain
+    p = make_panel(assets, days, seed=seed, tradable_p=0.9)
+    n_ad = int(p.valid.sum())
+    tm = {}
+    with threadpool_limits(1):                                       # 1 core, BLAS included
+        t0 = time.perf_counter()
+        pandas_chain.run_chain(p, "2006-12-29", "2007-12-31", timings=tm)
+        total = time.perf_counter() - t0
+    return {"value": round(n_ad / total, 1), "unit": "asset-days/s", "cores": 1, "kind": "port",
+            "sample": f"pandas/scikit-learn/SLSQP restatement of the reference call pattern "
+                      f"(oracle/pandas_chain.py) on {assets} assets x {days} days = {n_ad} "
+                      f"asset-days: " + ", ".join(f"{k} {v:.2f}s" for k, v in tm.items())
+                      + "; the reference as written measured 2,519 asset-days/s on 500 x 2,520 "
+                        "in the build container (SURVEY.md §6 F9)"}
+
+
+def cpu_port(seed: int, assets: int = 150, days: int = 2520):
+    """Secondary line: the vectorised oracle chain (oracle/chain.py: C factor restatement, numpy
+    z-score, scikit-learn Lasso, exact-QP PortfolioManager, analyzer, per-date FM lstsq), 1 core."""
     from threadpoolctl import threadpool_limits
 
     from afm.pipeline import FM30
@@ -73,7 +96,7 @@ def cpu_baseline(seed: int, assets: int = 150, days: int = 2520):
     p = make_panel(assets, days, seed=seed, tradable_p=0.9)
     n_ad = int(p.valid.sum())
     tm = {}
-    with threadpool_limits(1):                                       # 1 core, BLAS included
+    with threadpool_limits(1):
         t0 = time.perf_counter()
         chain.run_chain(p, "2006-12-29", "2007-12-31", fm_features=FM30, timings=tm)
         total = time.perf_counter() - t0
@@ -223,6 +246,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.seed)
+            res["cpu_baseline_port"] = cpu_port(args.seed)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
