@@ -22,7 +22,7 @@ import numpy as np
 from . import _lib
 
 V0 = 100000000
-MAX_BOOK = 64
+MAX_BOOK = 128
 
 
 def _dev():

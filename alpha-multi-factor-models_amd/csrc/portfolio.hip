@@ -30,7 +30,7 @@ namespace {
 
 typedef unsigned long long u64;
 constexpr int kT = 256;        // threads per workgroup
-constexpr int kMaxK = 64;      // max book size handled in LDS
+constexpr int kMaxK = 128;     // book-size cap; the global book arrays are [nd][2][kMaxK]
 constexpr int kMaxWords = 512; // lda <= 32768 assets
 
 struct RebArgs {
@@ -47,6 +47,7 @@ struct RebArgs {
     const double* tmr;        // [T][lda]
     int top_n;
     double lo, hi;
+    double* cov;              // scratch [nd][2][top_n][top_n]: each book's covariance
     // outputs (per rebalance date i)
     int32_t* k_out;           // [nd]
     int32_t* books;           // [nd][2][kMaxK] asset indices (long book, short book)
@@ -54,7 +55,7 @@ struct RebArgs {
     double* sums;             // [nd][4]: long_ret, short_ret, den_long, den_short
     int32_t* upos;            // [nd][2][2][kMaxK]: union position vs prev / vs next (-1 absent)
     int64_t* usize;           // [nd][2]: |P_prev U P_i|, |P_i U P_next|
-    int32_t* status;          // [nd]: 0 ok, 1 QP iteration cap, 2 k > kMaxK
+    int32_t* status;          // [nd] (zeroed by the launcher): |1 QP iteration cap, 2 k > cap
 };
 
 __device__ __forceinline__ u64 okey(double v) {   // order-preserving key, -0.0 == +0.0
@@ -84,25 +85,35 @@ __device__ int block_scan(int v, int* sbuf, int* excl) {
     return total;
 }
 
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// LDS of one (date, book) workgroup, sized for books of at most KM names.  The union holds the
+// history staging of the covariance phase, then the Cholesky slots of the QP (row q = member q;
+// L[q][q'] is meaningful for q' factored before q), or the tie buffer of the selection.
+template <int KM>
 struct Shared {
     u64 pw[3][kMaxWords];                // prediction presence rows: prev, cur, next
     int hist[256];
     int scan[kT];
     int misc[8];
-    u64 keysel[2 * kMaxK];
-    int idxsel[2 * kMaxK];
-    int book[2][kMaxK];
-    double S[kMaxK][kMaxK + 1];          // covariance of the current book
-    double L[kMaxK][kMaxK + 1];          // Cholesky work
-    double hv[kMaxK][65];                // staged history chunk [member][date]
-    double w[kMaxK], x[kMaxK], y1[kMaxK], y2[kMaxK], c[kMaxK], g[kMaxK];
-    int state[kMaxK], F[kMaxK];
-    double red[8];
+    u64 keysel[KM];
+    int idxsel[KM];
+    int book[KM];
+    int ord[KM], state[KM];              // QP: factor order (members), bound state per member
+    double w[KM], x[KM], c[KM];
+    union {
+        double hv[KM][65];               // staged history chunk [member][date]
+        double L[KM][KM + 1];            // Cholesky slots
+    } u;
 };
 
 // k largest keys among candidates (key valid when cand), ties -> smaller index first.
 // Writes the selected indices, sorted (key desc, index asc), to out[0..k).
-__device__ __forceinline__ void select_top(const RebArgs& r, Shared& sh, int64_t t, int k, bool largest, int* out) {
+template <int KM>
+__device__ __forceinline__ void select_top(const RebArgs& r, Shared<KM>& sh, int64_t t, int k,
+                                           bool largest, int* out) {
     const int tid = threadIdx.x;
     const int64_t A = r.A;
     u64 prefix = 0, pmask = 0;
@@ -180,7 +191,8 @@ __device__ __forceinline__ void select_top(const RebArgs& r, Shared& sh, int64_t
 // sum_{d' >= d} hist[d'] reaches `need` -> misc[0] = d, misc[1] = need - (count above d),
 // misc[2] = hist[d].  Lane l owns digits 4l..4l+3; a shuffle suffix scan replaces the serial
 // 256-step loop.
-__device__ __forceinline__ void digit_pick(Shared& sh, const int need) {
+template <int KM>
+__device__ __forceinline__ void digit_pick(Shared<KM>& sh, const int need) {
     const int tid = threadIdx.x;
     if (tid >= 64) return;
     const int h0 = sh.hist[4 * tid], h1 = sh.hist[4 * tid + 1], h2 = sh.hist[4 * tid + 2],
@@ -208,9 +220,9 @@ __device__ __forceinline__ void digit_pick(Shared& sh, const int need) {
 // select_top on register-resident keys: ks[j] = okey of asset j * kT + tid (0: not a candidate).
 // Same result as select_top (threshold by exact radix select; ties at the threshold taken by
 // ascending index), without re-reading the predictions for every digit.
-template <int KR>
-__device__ __forceinline__ bool select_top_reg(Shared& sh, const u64 (&ks)[KR], int k, bool largest,
-                                               int* out) {
+template <int KR, int KM>
+__device__ __forceinline__ bool select_top_reg(Shared<KM>& sh, const u64 (&ks)[KR], int k,
+                                               bool largest, int* out) {
     const int tid = threadIdx.x;
     u64 prefix = 0, pmask = 0;
     int need = k, eqtot = 0;
@@ -235,8 +247,8 @@ __device__ __forceinline__ bool select_top_reg(Shared& sh, const u64 (&ks)[KR], 
     }
     // keys > tau are all taken; of the eqtot keys == tau the `need` smallest indices (a tie
     // straddling the threshold is rare: its indices are ranked by counting in LDS)
-    int* eqbuf = reinterpret_cast<int*>(&sh.hv[0][0]);
-    constexpr int kEqMax = (int)(sizeof(sh.hv) / sizeof(int));
+    int* eqbuf = reinterpret_cast<int*>(&sh.u);
+    constexpr int kEqMax = (int)(sizeof(sh.u) / sizeof(int));
     const bool all_eq = eqtot == need;
     if (!all_eq && eqtot > kEqMax) return false;     // (uniform) caller takes the global path
     if (tid == 0) { sh.misc[3] = 0; sh.misc[6] = 0; }
@@ -306,136 +318,327 @@ __device__ double pairwise_dense(const double* a, int n) {
     return pairwise_dense(a, n2) + pairwise_dense(a + n2, n - n2);
 }
 
-// min w'Sw  s.t. sum w = 1, lo <= w <= hi for the n x n matrix in sh.S -> sh.w.  Primal active
-// set; each iteration solves [S_FF 1; 1' 0][w_F; lam] = [-S_FB w_B; b] by an LDS Cholesky of
-// S_FF and the Schur complement of the equality.  Returns true if the iteration cap was hit.
-// Called by every thread of the block.
-__device__ bool qp_solve(Shared& sh, const int n, const double lo, const double hi) {
-    const int tid = threadIdx.x;
+// ---- wave-level helpers of the QP (wave 0 runs it alone: no workgroup barrier inside) --------
+__device__ __forceinline__ double wave_sum(double v) {       // butterfly: identical in all lanes
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// lexicographic (v, code) minimum over the wave, in every lane
+__device__ __forceinline__ void wave_argmin(double& v, int& code) {
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double v2 = __shfl_xor(v, o, 64);
+        const int c2 = __shfl_xor(code, o, 64);
+        if (v2 < v || (v2 == v && c2 < code)) { v = v2; code = c2; }
+    }
+}
+
+__device__ __forceinline__ double rdlane(double v, int l) {   // l uniform
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// min w'Sw  s.t. sum w = 1, lo <= w <= hi for the n x n covariance S (global, row stride ld,
+// both triangles) -> sh.w, by the primal active-set method of oracle/portfolio.py:box_qp_weights
+// (KKT:811-833 solved exactly).  Each step solves [S_FF 1; 1' 0][w_F; lam] = [-S_FB w_B; b]
+// through a Cholesky factor of S_FF that is UPDATED, not refactored, as the free set changes:
+// a member bound by the ratio test leaves by a rank-1 update of the rows factored after it, a
+// member released by its multiplier joins as a new last row (one triangular solve).  All of it
+// runs on wave 0, lanes owning factor positions a = lane + 64 r; the sequential chains
+// (substitutions, the update sweep) broadcast one value per step with v_readlane.  Returns true
+// if the iteration cap was hit (uniform in wave 0); non-finite S -> NaN weights, capped.
+template <int KM>
+__device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const double* S, const int ld, const int n,
+                        const double lo, const double hi) {
+    constexpr int R = (KM + 63) / 64;
+    const int lane = threadIdx.x & 63;
+    double (*L)[KM + 1] = sh.u.L;
+    bool bad = false;
+    for (int e = lane; e < n * n; e += 64) bad |= !__builtin_isfinite(S[(e / n) * ld + e % n]);
+    if (__ballot(bad)) {
+        for (int q = lane; q < n; q += 64) sh.w[q] = __builtin_nan("");
+        lds_sync();
+        return true;
+    }
+    for (int q = lane; q < n; q += 64) {
+        sh.w[q] = 1.0 / n;
+        sh.state[q] = 0;
+        sh.ord[q] = q;
+    }
+    for (int e = lane; e < n * n; e += 64) {
+        const int a = e / n, b = e % n;
+        if (b <= a) L[a][b] = S[a * ld + b];
+    }
+    lds_sync();
+    for (int k = 0; k < n; ++k) {                      // right-looking Cholesky of S
+        const double d = __builtin_sqrt(L[k][k]);
+        lds_sync();
+        if (lane == 0) L[k][k] = d;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int a = lane + 64 * r;
+            if (a > k && a < n) L[a][k] = L[a][k] / d;
+        }
+        lds_sync();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int a = lane + 64 * r;
+            if (a > k && a < n) {
+                const double lak = L[a][k];
+                for (int b = k + 1; b <= a; ++b) L[a][b] = L[a][b] - lak * L[b][k];
+            }
+        }
+        lds_sync();
+    }
+
+    int nf = n;
     bool capped = false;
-    if (n > 0 && n * hi <= 1.0) {
-        if (tid < n) sh.w[tid] = hi;
-    } else if (n > 0 && n * lo >= 1.0) {
-        if (tid < n) sh.w[tid] = lo;
-    } else if (n > 0) {
-        if (tid < n) { sh.w[tid] = 1.0 / n; sh.state[tid] = 0; }
-        __syncthreads();
-        const int max_it = 4 * n + 8;
-        for (int it = 0; it < max_it; ++it) {
-            if (tid == 0) {
-                int nf = 0;
-                double bsum = 0.0;
-                for (int q = 0; q < n; ++q) {
-                    if (sh.state[q] == 0) sh.F[nf++] = q;
-                    else bsum = bsum + sh.w[q];
-                }
-                sh.misc[5] = nf;
-                sh.red[0] = 1.0 - bsum;
-            }
-            __syncthreads();
-            const int nf = sh.misc[5];
-            if (nf == 0) break;
-            if (it == max_it - 1) capped = true;
-            for (int e = tid; e < nf * nf; e += kT) {
-                int a = e / nf, b = e % nf;
-                sh.L[a][b] = sh.S[sh.F[a]][sh.F[b]];
-            }
-            if (tid < nf) {
-                double cc = 0.0;
+    const int max_it = 4 * n + 8;
+    for (int it = 0; it < max_it; ++it) {
+        if (nf == 0) break;
+        if (it == max_it - 1) capped = true;
+        int oq[R];
+        double y1[R], y2[R];
+        double bs = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int q = lane + 64 * r;
+            if (q < n && sh.state[q] != 0) bs += sh.w[q];
+            const int a = lane + 64 * r;
+            oq[r] = a < nf ? sh.ord[a] : 0;
+        }
+        const double bfree = 1.0 - wave_sum(bs);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {                  // c = S_FB w_B
+            double cc = 0.0;
+            if (lane + 64 * r < nf)
                 for (int q = 0; q < n; ++q)
-                    if (sh.state[q] != 0) cc = cc + sh.S[sh.F[tid]][q] * sh.w[q];
-                sh.c[tid] = cc;
-                sh.y1[tid] = 1.0;
-                sh.y2[tid] = cc;
-            }
-            __syncthreads();
-            for (int kk = 0; kk < nf; ++kk) {
-                if (tid == 0) sh.L[kk][kk] = __builtin_sqrt(sh.L[kk][kk]);
-                __syncthreads();
-                for (int a = kk + 1 + tid; a < nf; a += kT) sh.L[a][kk] = sh.L[a][kk] / sh.L[kk][kk];
-                __syncthreads();
-                const int m = nf - kk - 1;
-                for (int e = tid; e < m * m; e += kT) {
-                    int a = kk + 1 + e / m, b = kk + 1 + e % m;
-                    if (b <= a) sh.L[a][b] = sh.L[a][b] - sh.L[a][kk] * sh.L[b][kk];
-                }
-                __syncthreads();
-            }
-            if (tid < 2) {
-                double* y = tid == 0 ? sh.y1 : sh.y2;
-                for (int a = 0; a < nf; ++a) {
-                    double s = y[a];
-                    for (int b = 0; b < a; ++b) s = s - sh.L[a][b] * y[b];
-                    y[a] = s / sh.L[a][a];
-                }
-                for (int a = nf - 1; a >= 0; --a) {
-                    double s = y[a];
-                    for (int b = a + 1; b < nf; ++b) s = s - sh.L[b][a] * y[b];
-                    y[a] = s / sh.L[a][a];
+                    if (sh.state[q] != 0) cc = cc + S[q * ld + oq[r]] * sh.w[q];
+            y1[r] = 1.0;
+            y2[r] = cc;
+        }
+        // S_FF y = rhs for both right-hand sides: forward (L) then backward (L')
+        for (int b = 0; b < nf; ++b) {
+            const int rb = b >> 6, lb = b & 63;
+            const int qb = sh.ord[b];
+            const double lbb = L[qb][qb];
+            double v1 = 0.0, v2 = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (r == rb) {
+                    if (lane == lb) { y1[r] = y1[r] / lbb; y2[r] = y2[r] / lbb; }
+                    v1 = rdlane(y1[r], lb);
+                    v2 = rdlane(y2[r], lb);
                 }
             }
-            __syncthreads();
-            if (tid == 0) {
-                double s1 = 0.0, s2 = 0.0;
-                for (int a = 0; a < nf; ++a) { s1 = s1 + sh.y1[a]; s2 = s2 + sh.y2[a]; }
-                const double lam = -(sh.red[0] + s2) / s1;
-                int feas = 1;
-                for (int a = 0; a < nf; ++a) {
-                    double xv = -sh.y2[a] - lam * sh.y1[a];
-                    sh.x[a] = xv;
-                    if (!(xv >= lo) || !(xv <= hi)) feas = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int a = lane + 64 * r;
+                if (a > b && a < nf) {
+                    const double l = L[oq[r]][qb];
+                    y1[r] = y1[r] - l * v1;
+                    y2[r] = y2[r] - l * v2;
                 }
-                int done = 0;
-                if (feas) {
-                    for (int a = 0; a < nf; ++a) sh.w[sh.F[a]] = sh.x[a];
-                    int jmin = -1;
-                    double vmin = 0.0;
-                    for (int q = 0; q < n; ++q) {
-                        if (sh.state[q] == 0) continue;
-                        double gq = 0.0;
-                        for (int b = 0; b < n; ++b) gq = gq + sh.S[q][b] * sh.w[b];
-                        gq = gq + lam;
-                        const double v = sh.state[q] < 0 ? gq : -gq;
-                        if (v < vmin) { vmin = v; jmin = q; }
+            }
+        }
+        for (int a = nf - 1; a >= 0; --a) {
+            const int ra = a >> 6, la = a & 63;
+            const int qa = sh.ord[a];
+            const double laa = L[qa][qa];
+            double v1 = 0.0, v2 = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (r == ra) {
+                    if (lane == la) { y1[r] = y1[r] / laa; y2[r] = y2[r] / laa; }
+                    v1 = rdlane(y1[r], la);
+                    v2 = rdlane(y2[r], la);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int b = lane + 64 * r;
+                if (b < a) {
+                    const double l = L[qa][oq[r]];
+                    y1[r] = y1[r] - l * v1;
+                    y2[r] = y2[r] - l * v2;
+                }
+            }
+        }
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (lane + 64 * r < nf) { s1 += y1[r]; s2 += y2[r]; }
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        const double lam = -(bfree + s2) / s1;
+        double x[R];
+        bool infeas = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            x[r] = -y2[r] - lam * y1[r];
+            if (lane + 64 * r < nf && (!(x[r] >= lo) || !(x[r] <= hi))) infeas = true;
+        }
+        if (!__ballot(infeas)) {
+            // feasible: take x; release the bound member with the most negative multiplier
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (lane + 64 * r < nf) sh.w[oq[r]] = x[r];
+            lds_sync();
+            double vmin = __builtin_inf();
+            int qmin = 0x7fffffff;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int q = lane + 64 * r;
+                if (q < n && sh.state[q] != 0) {
+                    double g = 0.0;
+                    for (int b = 0; b < n; ++b) g = g + S[q * ld + b] * sh.w[b];
+                    g = g + lam;
+                    const double v = sh.state[q] < 0 ? g : -g;
+                    if (v < vmin) { vmin = v; qmin = q; }
+                }
+            }
+            wave_argmin(vmin, qmin);
+            if (!(vmin < 0.0)) break;
+            // qmin joins the free set as the last factor row: l = L^-1 S[F][qmin]
+            double l[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) l[r] = lane + 64 * r < nf ? S[qmin * ld + oq[r]] : 0.0;
+            for (int b = 0; b < nf; ++b) {
+                const int rb = b >> 6, lb = b & 63;
+                const int qb = sh.ord[b];
+                const double lbb = L[qb][qb];
+                double v = 0.0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (r == rb) {
+                        if (lane == lb) l[r] = l[r] / lbb;
+                        v = rdlane(l[r], lb);
                     }
-                    if (jmin < 0) done = 1;
-                    else sh.state[jmin] = 0;
-                } else {
-                    double alpha = 1.0;
-                    int jb = -1, bound = 0;
-                    for (int a = 0; a < nf; ++a) {
-                        const int q = sh.F[a];
-                        const double pq = sh.x[a] - sh.w[q];
-                        if (sh.x[a] < lo && pq < 0) {
-                            const double al = (lo - sh.w[q]) / pq;
-                            if (al < alpha) { alpha = al; jb = q; bound = -1; }
-                        } else if (sh.x[a] > hi && pq > 0) {
-                            const double al = (hi - sh.w[q]) / pq;
-                            if (al < alpha) { alpha = al; jb = q; bound = 1; }
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int a = lane + 64 * r;
+                    if (a > b && a < nf) l[r] = l[r] - L[oq[r]][qb] * v;
+                }
+            }
+            double ss = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (lane + 64 * r < nf) {
+                    L[qmin][oq[r]] = l[r];
+                    ss += l[r] * l[r];
+                }
+            ss = wave_sum(ss);
+            lds_sync();
+            if (lane == 0) {
+                L[qmin][qmin] = __builtin_sqrt(S[qmin * ld + qmin] - ss);
+                sh.ord[nf] = qmin;
+                sh.state[qmin] = 0;
+            }
+            lds_sync();
+            ++nf;
+        } else {
+            // ratio test: the first member (ascending index) to hit its bound along x - w
+            double amin = __builtin_inf();
+            int code = 0x7fffffff;                     // 2 * member + (bound is hi)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (lane + 64 * r < nf) {
+                    const int q = oq[r];
+                    const double wq = sh.w[q];
+                    const double pq = x[r] - wq;
+                    if (x[r] < lo && pq < 0) {
+                        const double al = (lo - wq) / pq;
+                        if (al < 1.0 && (al < amin || (al == amin && 2 * q < code))) {
+                            amin = al;
+                            code = 2 * q;
+                        }
+                    } else if (x[r] > hi && pq > 0) {
+                        const double al = (hi - wq) / pq;
+                        if (al < 1.0 && (al < amin || (al == amin && 2 * q + 1 < code))) {
+                            amin = al;
+                            code = 2 * q + 1;
                         }
                     }
-                    for (int a = 0; a < nf; ++a) {
-                        const int q = sh.F[a];
-                        sh.w[q] = sh.w[q] + alpha * (sh.x[a] - sh.w[q]);
-                    }
-                    if (jb >= 0) {
-                        sh.w[jb] = bound < 0 ? lo : hi;
-                        sh.state[jb] = bound;
+                }
+            }
+            wave_argmin(amin, code);
+            const bool hit = code != 0x7fffffff;
+            const double alpha = hit ? amin : 1.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (lane + 64 * r < nf) {
+                    const double wq = sh.w[oq[r]];
+                    sh.w[oq[r]] = wq + alpha * (x[r] - wq);
+                }
+            lds_sync();
+            if (hit) {
+                const int jb = code >> 1;
+                if (lane == 0) {
+                    sh.w[jb] = (code & 1) ? hi : lo;
+                    sh.state[jb] = (code & 1) ? 1 : -1;
+                }
+                // factor position of jb; rows after it absorb its column (rank-1 update)
+                int j = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const u64 m = __ballot(lane + 64 * r < nf && oq[r] == jb);
+                    if (m) j = 64 * r + __builtin_ctzll(m);
+                }
+                double xv[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int a = lane + 64 * r;
+                    xv[r] = (a > j && a < nf) ? L[oq[r]][jb] : 0.0;
+                }
+                for (int k = j + 1; k < nf; ++k) {
+                    const int rk = k >> 6, lk = k & 63;
+                    const int qk = sh.ord[k];
+                    const double lkk = L[qk][qk];
+                    double xk = 0.0;
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        if (r == rk) xk = rdlane(xv[r], lk);
+                    const double rr = __builtin_sqrt(lkk * lkk + xk * xk);
+                    const double cs = rr / lkk, sn = xk / lkk;
+                    lds_sync();
+                    if (lane == 0) L[qk][qk] = rr;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int a = lane + 64 * r;
+                        if (a > k && a < nf) {
+                            const double ln = (L[oq[r]][qk] + sn * xv[r]) / cs;
+                            L[oq[r]][qk] = ln;
+                            xv[r] = cs * xv[r] - sn * ln;
+                        }
                     }
                 }
-                sh.misc[7] = done;
+                int nxt[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int a = lane + 64 * r;
+                    nxt[r] = (a >= j && a + 1 < nf) ? sh.ord[a + 1] : -1;
+                }
+                lds_sync();
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (nxt[r] >= 0) sh.ord[lane + 64 * r] = nxt[r];
+                lds_sync();
+                --nf;
             }
-            __syncthreads();
-            if (sh.misc[7]) break;
         }
     }
-    __syncthreads();
+    lds_sync();
     return capped;
 }
 
 // Welford pairwise-complete covariance (pandas nancorr, cov=True) of a dense [rows][ld] matrix
-// (k columns, NaN = missing) into sh.S; rows staged 64 at a time.
-__device__ void dense_cov(Shared& sh, const double* R, int64_t rows, int64_t ld, int k) {
+// (k columns, NaN = missing) into S [k][k]; rows staged 64 at a time.
+template <int KM>
+__device__ __forceinline__ void dense_cov(Shared<KM>& sh, const double* R, int64_t rows, int64_t ld, int k,
+                          double* S) {
     const int tid = threadIdx.x;
     const int npairs = k * (k + 1) / 2;
     for (int pb = 0; pb < npairs; pb += kT) {
@@ -451,13 +654,13 @@ __device__ void dense_cov(Shared& sh, const double* R, int64_t rows, int64_t ld,
             __syncthreads();
             for (int e = tid; e < k * 64; e += kT) {
                 const int m = e / 64, d = e % 64;
-                sh.hv[m][d] = (h0 + d < rows) ? R[(h0 + d) * ld + m] : __builtin_nan("");
+                sh.u.hv[m][d] = (h0 + d < rows) ? R[(h0 + d) * ld + m] : __builtin_nan("");
             }
             __syncthreads();
             if (pq < npairs) {
                 const int nd = (int)((rows - h0) < 64 ? (rows - h0) : 64);
                 for (int d = 0; d < nd; ++d) {
-                    const double vx = sh.hv[pi][d], vy = sh.hv[pj][d];
+                    const double vx = sh.u.hv[pi][d], vy = sh.u.hv[pj][d];
                     if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
                         nobs += 1;
                         const double dx = vx - mx, dy = vy - my;
@@ -471,31 +674,43 @@ __device__ void dense_cov(Shared& sh, const double* R, int64_t rows, int64_t ld,
         if (pq < npairs) {
             double cv = __builtin_nan("");
             if (nobs >= 1 && (nobs - 1.0) != 0) cv = cxy / (nobs - 1.0);
-            sh.S[pi][pj] = cv;
-            sh.S[pj][pi] = cv;
+            S[pi * k + pj] = cv;
+            S[pj * k + pi] = cv;
         }
     }
     __syncthreads();
 }
 
+// determine_weights for one book: covariance into `cov` (an output), then the QP reading it
 __global__ __launch_bounds__(kT) void weights_kernel(const double* R, int64_t rows, int64_t ld,
                                                      int k, double lo, double hi, double* w,
                                                      double* cov, int32_t* status) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    Shared& sh = *reinterpret_cast<Shared*>(smem_raw);
-    dense_cov(sh, R, rows, ld, k);
-    const bool capped = qp_solve(sh, k, lo, hi);
+    Shared<kMaxK>& sh = *reinterpret_cast<Shared<kMaxK>*>(smem_raw);
+    dense_cov(sh, R, rows, ld, k, cov);
     const int tid = threadIdx.x;
+    bool capped = false;
+    if (k * hi <= 1.0) {
+        if (tid < k) sh.w[tid] = hi;
+    } else if (k * lo >= 1.0) {
+        if (tid < k) sh.w[tid] = lo;
+    } else if (tid < 64) {
+        capped = qp_wave(sh, cov, k, k, lo, hi);
+    }
+    __syncthreads();
     if (tid < k) w[tid] = sh.w[tid];
-    for (int e = tid; e < k * k; e += kT) cov[e] = sh.S[e / k][e % k];
     if (tid == 0) status[0] = capped ? 1 : 0;
 }
 
+// One workgroup per (rebalance date i = blockIdx.x, book side = blockIdx.y): side 0 the long
+// book (k largest predictions), side 1 the short book (k smallest).
+template <int KM>
 __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    Shared& sh = *reinterpret_cast<Shared*>(smem_raw);
+    Shared<KM>& sh = *reinterpret_cast<Shared<KM>*>(smem_raw);
     const int tid = threadIdx.x;
     const int64_t i = blockIdx.x;
+    const int side = blockIdx.y;
     const int64_t t = r.dates[i];
     const int64_t tp = i > 0 ? r.dates[i - 1] : -1;
     const int64_t tn = i + 1 < r.nd ? r.dates[i + 1] : -1;
@@ -545,115 +760,117 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
     }
     int ex;
     const int ncand = block_scan(nc, sh.scan, &ex);
-    int k = ncand < 2 * r.top_n ? ncand / 2 : r.top_n;
-    if (k > kMaxK) {
-        if (tid == 0) { r.status[i] = 2; r.k_out[i] = k; }
+    const int k = ncand < 2 * r.top_n ? ncand / 2 : r.top_n;
+    if (k > KM) {
+        if (tid == 0) { r.status[i] = 2; if (side == 0) r.k_out[i] = k; }
         return;
     }
-    if (tid == 0) { r.k_out[i] = k; r.status[i] = 0; }
+    if (tid == 0 && side == 0) r.k_out[i] = k;
 
+    const bool largest = side == 0;
     if (k > 0 && regk) {
-        if (!select_top_reg<KR>(sh, ks, k, true, sh.book[0]))
-            select_top(r, sh, t, k, true, sh.book[0]);
-        if (!select_top_reg<KR>(sh, ks, k, false, sh.book[1]))
-            select_top(r, sh, t, k, false, sh.book[1]);
+        if (!select_top_reg<KR>(sh, ks, k, largest, sh.book))
+            select_top(r, sh, t, k, largest, sh.book);
     } else if (k > 0) {
-        select_top(r, sh, t, k, true, sh.book[0]);
-        select_top(r, sh, t, k, false, sh.book[1]);
+        select_top(r, sh, t, k, largest, sh.book);
     }
     __syncthreads();
 
-    if (tid == 0) sh.misc[4] = 0;
     const int64_t hlo = r.window > 0 ? (t - r.window > 0 ? t - r.window : 0) : r.h_t0;
     const int64_t hhi = r.window > 0 ? t : r.h_t1;
-    for (int side = 0; side < 2; ++side) {
-        const int* bk = sh.book[side];
-        // ---- pairwise-complete covariance (pandas nancorr, cov=True) ----------------------
-        const int npairs = k * (k + 1) / 2;
-        for (int pb = 0; pb < npairs; pb += kT) {
-            const int pq = pb + tid;
-            int pi = 0, pj = 0;
-            if (pq < npairs) {   // pq -> (xi >= yi) in row-major lower-triangle order
-                int q = pq;
-                pi = 0;
-                while (q > pi) { q -= pi + 1; ++pi; }
-                pj = q;
+    const int* bk = sh.book;
+    double* S = r.cov + (i * 2 + side) * (int64_t)r.top_n * r.top_n;
+    // ---- pairwise-complete covariance (pandas nancorr, cov=True), into the scratch S ----------
+    const int npairs = k * (k + 1) / 2;
+    for (int pb = 0; pb < npairs; pb += kT) {
+        const int pq = pb + tid;
+        int pi = 0, pj = 0;
+        if (pq < npairs) {   // pq -> (xi >= yi) in row-major lower-triangle order
+            int q = pq;
+            pi = 0;
+            while (q > pi) { q -= pi + 1; ++pi; }
+            pj = q;
+        }
+        double nobs = 0, mx = 0, my = 0, cxy = 0;
+        for (int64_t h0 = hlo; h0 < hhi; h0 += 64) {
+            __syncthreads();
+            for (int e = tid; e < k * 64; e += kT) {
+                int m = e / 64, d = e % 64;
+                int64_t th = h0 + d;
+                double v = __builtin_nan("");
+                if (th < hhi && bit_at(r.hbits, r.lda, th, bk[m])) v = r.hist[th * r.lda + bk[m]];
+                sh.u.hv[m][d] = v;
             }
-            double nobs = 0, mx = 0, my = 0, cxy = 0;
-            for (int64_t h0 = hlo; h0 < hhi; h0 += 64) {
-                __syncthreads();
-                for (int e = tid; e < k * 64; e += kT) {
-                    int m = e / 64, d = e % 64;
-                    int64_t th = h0 + d;
-                    double v = __builtin_nan("");
-                    if (th < hhi && bit_at(r.hbits, r.lda, th, bk[m])) v = r.hist[th * r.lda + bk[m]];
-                    sh.hv[m][d] = v;
-                }
-                __syncthreads();
-                if (pq < npairs) {
-                    const int nd = (int)((hhi - h0) < 64 ? (hhi - h0) : 64);
-                    for (int d = 0; d < nd; ++d) {
-                        double vx = sh.hv[pi][d], vy = sh.hv[pj][d];
-                        if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
-                            nobs += 1;
-                            double dx = vx - mx, dy = vy - my;
-                            mx += 1. / nobs * dx;
-                            my += 1. / nobs * dy;
-                            cxy += (vx - mx) * dy;
-                        }
+            __syncthreads();
+            if (pq < npairs) {
+                const int nd = (int)((hhi - h0) < 64 ? (hhi - h0) : 64);
+                for (int d = 0; d < nd; ++d) {
+                    double vx = sh.u.hv[pi][d], vy = sh.u.hv[pj][d];
+                    if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
+                        nobs += 1;
+                        double dx = vx - mx, dy = vy - my;
+                        mx += 1. / nobs * dx;
+                        my += 1. / nobs * dy;
+                        cxy += (vx - mx) * dy;
                     }
                 }
             }
-            if (pq < npairs) {
-                double cv = __builtin_nan("");
-                if (nobs >= 1 && (nobs - 1.0) != 0) cv = cxy / (nobs - 1.0);
-                sh.S[pi][pj] = cv;
-                sh.S[pj][pi] = cv;
-            }
         }
-        __syncthreads();
-
-        // ---- exact box-constrained QP (primal active set) --------------------------------
-        if (qp_solve(sh, k, r.lo, r.hi) && tid == 0) sh.misc[4] = 1;
-        __syncthreads();
-        // ---- outputs for this book -------------------------------------------------------
-        double* wout = r.weights + (i * 2 + side) * kMaxK;
-        int32_t* bout = r.books + (i * 2 + side) * kMaxK;
-        if (tid < k) {
-            wout[tid] = sh.w[tid];
-            bout[tid] = bk[tid];
-            sh.x[tid] = r.tmr[t * r.lda + bk[tid]] * sh.w[tid];   // tmr * w (book order)
-            sh.x[tid] = sh.x[tid] == sh.x[tid] ? sh.x[tid] : 0.0;  // nansum
-            sh.c[tid] = sh.w[tid] * r.close[t * r.lda + bk[tid]];   // w * price
+        if (pq < npairs) {
+            double cv = __builtin_nan("");
+            if (nobs >= 1 && (nobs - 1.0) != 0) cv = cxy / (nobs - 1.0);
+            S[pi * k + pj] = cv;
+            S[pj * k + pi] = cv;
         }
-        __syncthreads();
-        if (tid == 0) {
-            r.sums[i * 4 + side] = pairwise_dense(sh.x, k);
-            double den = 0.0;                                       // builtin sum(): 0 + ...
-            for (int a = 0; a < k; ++a) den = den + sh.c[a];
-            r.sums[i * 4 + 2 + side] = den;
-            if (sh.misc[4]) r.status[i] = 1;
-        }
-        // union positions of the members vs the previous / next rebalance date
-        if (tid < k) {
-            const int a = bk[tid];
-            const int wa = a >> 6, ba = a & 63;
-            for (int q = 0; q < 2; ++q) {
-                const int other = q == 0 ? 0 : 2;                   // prev row / next row
-                const bool has = (q == 0 ? tp : tn) >= 0 && ((sh.pw[other][wa] >> ba) & 1ull);
-                int pos = -1;
-                if (has) {
-                    pos = 0;
-                    for (int wi = 0; wi < wa; ++wi) pos += __popcll(sh.pw[other][wi] | sh.pw[1][wi]);
-                    u64 lowm = ba ? ((1ull << ba) - 1ull) : 0ull;
-                    pos += __popcll((sh.pw[other][wa] | sh.pw[1][wa]) & lowm);
-                }
-                r.upos[((i * 2 + side) * 2 + q) * kMaxK + tid] = pos;
-            }
-        }
-        __syncthreads();
     }
-    if (tid < 2) {
+    __syncthreads();
+
+    // ---- exact box-constrained QP (primal active set, wave 0) -----------------------------
+    bool capped = false;
+    if (k > 0 && k * r.hi <= 1.0) {
+        if (tid < k) sh.w[tid] = r.hi;
+    } else if (k > 0 && k * r.lo >= 1.0) {
+        if (tid < k) sh.w[tid] = r.lo;
+    } else if (k > 0 && tid < 64) {
+        capped = qp_wave(sh, S, k, k, r.lo, r.hi);
+    }
+    if (capped && tid == 0) atomicOr(&r.status[i], 1);
+    __syncthreads();
+    // ---- outputs for this book -----------------------------------------------------------
+    double* wout = r.weights + (i * 2 + side) * kMaxK;
+    int32_t* bout = r.books + (i * 2 + side) * kMaxK;
+    if (tid < k) {
+        wout[tid] = sh.w[tid];
+        bout[tid] = bk[tid];
+        const double tw = r.tmr[t * r.lda + bk[tid]] * sh.w[tid];   // tmr * w (book order)
+        sh.x[tid] = tw == tw ? tw : 0.0;                            // nansum
+        sh.c[tid] = sh.w[tid] * r.close[t * r.lda + bk[tid]];       // w * price
+    }
+    __syncthreads();
+    if (tid == 0) {
+        r.sums[i * 4 + side] = pairwise_dense(sh.x, k);
+        double den = 0.0;                                           // builtin sum(): 0 + ...
+        for (int a = 0; a < k; ++a) den = den + sh.c[a];
+        r.sums[i * 4 + 2 + side] = den;
+    }
+    // union positions of the members vs the previous / next rebalance date
+    if (tid < k) {
+        const int a = bk[tid];
+        const int wa = a >> 6, ba = a & 63;
+        for (int q = 0; q < 2; ++q) {
+            const int other = q == 0 ? 0 : 2;                       // prev row / next row
+            const bool has = (q == 0 ? tp : tn) >= 0 && ((sh.pw[other][wa] >> ba) & 1ull);
+            int pos = -1;
+            if (has) {
+                pos = 0;
+                for (int wi = 0; wi < wa; ++wi) pos += __popcll(sh.pw[other][wi] | sh.pw[1][wi]);
+                u64 lowm = ba ? ((1ull << ba) - 1ull) : 0ull;
+                pos += __popcll((sh.pw[other][wa] | sh.pw[1][wa]) & lowm);
+            }
+            r.upos[((i * 2 + side) * 2 + q) * kMaxK + tid] = pos;
+        }
+    }
+    if (side == 0 && tid < 2) {
         const int other = tid == 0 ? 0 : 2;
         int64_t tot = 0;
         for (int wi = 0; wi < nw; ++wi) tot += __popcll(sh.pw[other][wi] | sh.pw[1][wi]);
@@ -824,10 +1041,6 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
 
 constexpr int kChunkDates = 64;
 constexpr int kBufWords = 12288;
-
-__device__ __forceinline__ void lds_sync() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
 
 // One workgroup of 2 waves.  Wave 1 stages chunk c+1 (records + sums) into LDS while wave 0
 // runs chunk c; one barrier per chunk.  Wave 0 keeps V / V_prev replicated in every lane.
@@ -1034,6 +1247,17 @@ __global__ __launch_bounds__(64) void pair_union_kernel(int64_t steps, const int
 
 using namespace afm;
 
+template <int KM>
+static int launch_rebalance(afm_ctx* ctx, const RebArgs& r) {
+    const size_t smem = sizeof(Shared<KM>);
+    AFM_HIP(hipFuncSetAttribute((const void*)rebalance_kernel<KM>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    hipLaunchKernelGGL(rebalance_kernel<KM>, dim3((unsigned)r.nd, 2), dim3(kT), smem, ctx->stream,
+                       r);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
 extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                                  const int32_t* dates, int64_t nd, const double* pred,
                                  const uint64_t* trad_bits, const double* hist,
@@ -1045,19 +1269,20 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
     AFM_CTX(ctx);
     AFM_CHECK_ARG(T > 0 && A > 0 && lda >= A && lda % 64 == 0, "bad panel shape");
     AFM_CHECK_ARG((A + 63) / 64 <= kMaxWords, "too many assets (max 32768)");
-    AFM_CHECK_ARG(top_n >= 0 && top_n <= kMaxK, "top_n must be in [0, 64]");
+    AFM_CHECK_ARG(top_n >= 0 && top_n <= kMaxK, "top_n must be in [0, 128]");
     AFM_CHECK_ARG(dates && pred && trad_bits && hist && hist_bits && close && tmr && k_out &&
                       books && weights && sums && upos && usize && status, "null buffer");
     AFM_CHECK_ARG(lo <= hi, "lo > hi");
     if (nd <= 0) return AFM_OK;
+    double* cov = nullptr;
+    const size_t b_cov = sizeof(double) * (size_t)nd * 2 * ((size_t)top_n * top_n + 1);
+    AFM_HIP(hipMallocAsync((void**)&cov, b_cov, ctx->stream));
+    AFM_HIP(hipMemsetAsync(status, 0, sizeof(int32_t) * (size_t)nd, ctx->stream));
     RebArgs r{T, lda, A, dates, nd, pred, trad_bits, hist, hist_bits, h_t0, h_t1, window, close,
-              tmr, top_n, lo, hi, k_out, books, weights, sums, upos, usize, status};
-    const size_t smem = sizeof(Shared);
-    AFM_HIP(hipFuncSetAttribute((const void*)rebalance_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-    hipLaunchKernelGGL(rebalance_kernel, dim3((unsigned)nd), dim3(kT), smem, ctx->stream, r);
-    AFM_HIP(hipGetLastError());
-    return AFM_OK;
+              tmr, top_n, lo, hi, cov, k_out, books, weights, sums, upos, usize, status};
+    const int rc = top_n <= 32 ? launch_rebalance<32>(ctx, r) : launch_rebalance<kMaxK>(ctx, r);
+    AFM_HIP(hipFreeAsync(cov, ctx->stream));
+    return rc;
 }
 
 extern "C" int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out,
@@ -1086,9 +1311,9 @@ extern "C" int afm_min_variance_weights_f64(afm_ctx* ctx, const double* R, int64
                                             int64_t ld, int k, double lo, double hi, double* w,
                                             double* cov, int32_t* status) {
     AFM_CTX(ctx);
-    AFM_CHECK_ARG(k >= 1 && k <= kMaxK && ld >= k && rows >= 0, "need 1 <= k <= 64, ld >= k");
+    AFM_CHECK_ARG(k >= 1 && k <= kMaxK && ld >= k && rows >= 0, "need 1 <= k <= 128, ld >= k");
     AFM_CHECK_ARG(R && w && cov && status && lo <= hi, "bad arguments");
-    const size_t smem = sizeof(Shared);
+    const size_t smem = sizeof(Shared<kMaxK>);
     AFM_HIP(hipFuncSetAttribute((const void*)weights_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
     hipLaunchKernelGGL(weights_kernel, dim3(1), dim3(kT), smem, ctx->stream, R, rows, ld, k, lo,

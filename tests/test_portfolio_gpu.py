@@ -184,3 +184,70 @@ def test_bootstrap_paths_vs_oracle(top_n, window, npaths):
     v = np.asarray(pm.portfolio_value["Portfolio"], dtype=np.float64)
     assert same(got["value"][2], v)
     assert same(got["turnover"][2, 1:], np.asarray(pm.turnovers[1:], dtype=np.float64))
+
+
+@pytest.mark.parametrize("k,holes", [(64, False), (100, False), (100, True), (128, False)])
+def test_large_book_weights_vs_oracle(k, holes):
+    """determine_weights for the survey's stress book sizes (top_n = 100): the
+    active-set QP with its incrementally updated Cholesky factor against the oracle's
+    refactor-every-step solve, rel 1e-9; identical bound sets."""
+    from afm.portfolio import min_variance_weights
+    from oracle import portfolio as P
+    rng = np.random.default_rng(k + holes)
+    rows = 260
+    f = rng.normal(0, 0.01, (rows, 4))                       # a few common factors + noise
+    scale = rng.uniform(0.3, 2, k)
+    scale[:3] = 0.05                                         # low-vol names: pinned at hi
+    R = f @ rng.normal(0, 0.2, (4, k)) + rng.normal(0, 0.02, (rows, k)) * scale
+    if holes:
+        R[rng.random(R.shape) < 0.01] = np.nan
+    w, cov = min_variance_weights(R)
+    S = P.pairwise_cov(R)
+    assert np.abs(cov - S).max() <= 1e-12 * np.abs(S).max()
+    wo, it = P.box_qp_weights(S)
+    assert it >= 3                                           # the active set really iterates
+    assert (wo >= 0.1 - 1e-14).any() and (wo <= 1e-14).any()    # both bounds active
+    assert np.array_equal(w <= 1e-14, wo <= 1e-14)
+    assert np.array_equal(w >= 0.1 - 1e-14, wo >= 0.1 - 1e-14)
+    assert np.abs(w - wo).max() < 1e-9
+    assert abs(w.sum() - 1) < 1e-12
+
+
+def test_top100_books_weights_pnl_vs_oracle():
+    """Rebalance at top_n = 100 (the stress book, KKT:796 parameterised): books identical, weights
+    rel 1e-9 against the exact-QP oracle, the value path rel 1e-12."""
+    from afm.portfolio import PortfolioManager
+    from oracle import portfolio as P
+    rng = np.random.default_rng(100)
+    T, A, top_n = 190, 420, 100
+    dates = np.asarray(np.busday_offset(np.datetime64("2016-01-04"), np.arange(T), roll="forward"),
+                       dtype="datetime64[ns]")
+    ids = 11 + 3 * np.arange(A)
+    present = rng.random((T, A)) < 0.97
+    present[:170] = True                                     # complete history: np.cov path
+    tt, aa = np.nonzero(present)
+    d, i = dates[tt], ids[aa]
+    f = rng.normal(0, 0.01, (T, 3))
+    ret = (f @ rng.normal(0, 1, (3, A)))[tt, aa] + rng.normal(0, 0.02, len(tt))
+    close = 50 * np.exp(rng.normal(0, 0.1, len(tt)))
+    trad = rng.random(len(tt)) < 0.95
+    hist_m = tt < 170
+    test_m = tt >= 170
+    pred_v = rng.normal(size=test_m.sum())
+    pred = pd.DataFrame({"p": pred_v}, index=pd.MultiIndex.from_arrays([d[test_m], i[test_m]]))
+    hist = pd.DataFrame({"target": ret[hist_m]}, index=pd.MultiIndex.from_arrays([d[hist_m], i[hist_m]]))
+    all_df = pd.DataFrame({"in_trading_universe": np.where(trad, "Y", "N"), "close_price": close,
+                           "tmr_ret1d": ret}, index=pd.MultiIndex.from_arrays([d, i]))
+    pm = PortfolioManager(pred, hist, all_df, top_n=top_n, window=120)
+    pm.calculate_portfolio()
+    o = P.run_portfolio(d[test_m].astype(np.int64), i[test_m], pred_v,
+                        d[hist_m].astype(np.int64), i[hist_m], ret[hist_m],
+                        d.astype(np.int64), i, trad, close, ret, top_n=top_n, window=120)
+    for (dt, L, S), Lo, So in zip(pm.books, o["books"][0::2], o["books"][1::2]):
+        assert len(L) == top_n
+        assert L == Lo.tolist() and S == So.tolist()
+    for j, (wol, wos) in enumerate(zip(o["weights"][0::2], o["weights"][1::2])):
+        assert np.abs(pm.weights[j, 0, :top_n] - wol).max() < 1e-9
+        assert np.abs(pm.weights[j, 1, :top_n] - wos).max() < 1e-9
+    v = np.asarray(pm.portfolio_value["Portfolio"], dtype=np.float64)
+    assert np.abs(v - o["value"]).max() / o["value"].max() < 1e-12
