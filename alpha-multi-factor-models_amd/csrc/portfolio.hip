@@ -23,6 +23,8 @@
 //   -> 0 included, evaluated sparsely at the members' union positions).
 #include "afm_internal.h"
 
+#include <vector>
+
 #pragma clang fp contract(off)
 
 namespace afm {
@@ -47,7 +49,10 @@ struct RebArgs {
     const double* tmr;        // [T][lda]
     int top_n;
     double lo, hi;
-    double* cov;              // scratch [nd][2][top_n][top_n]: each book's covariance
+    double* hscr;             // scratch [nd][2][top_n][hrows]: books' history windows (or null)
+    int64_t hrows;            // rows per window: window, or h_t1 - h_t0
+    int probe;                // experiments (AFM_REB_PROBE): 1 skip the QP, 2 skip the covariance,
+    int64_t* stamps;          // 4 phase timestamps per workgroup ([nd][2][5])
     // outputs (per rebalance date i)
     int32_t* k_out;           // [nd]
     int32_t* books;           // [nd][2][kMaxK] asset indices (long book, short book)
@@ -89,9 +94,16 @@ __device__ __forceinline__ void lds_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-// LDS of one (date, book) workgroup, sized for books of at most KM names.  The union holds the
-// history staging of the covariance phase, then the Cholesky slots of the QP (row q = member q;
-// L[q][q'] is meaningful for q' factored before q), or the tie buffer of the selection.
+// packed symmetric index of the member pair (a, b)
+__device__ __forceinline__ int tri(int a, int b) {
+    return a >= b ? a * (a + 1) / 2 + b : b * (b + 1) / 2 + a;
+}
+
+// LDS of one (date, book) workgroup, sized for books of at most KM names: the covariance S
+// (packed, tri()), and a union of the history staging of the covariance phase, the Cholesky
+// factor of the QP or the tie buffer of the selection.  The factor is packed by member PAIR: the
+// entry of {q, q'} belongs to whichever of the two was factored later (row) -- one orientation
+// per pair -- so members can leave and join the factor order without moving data.
 template <int KM>
 struct Shared {
     u64 pw[3][kMaxWords];                // prediction presence rows: prev, cur, next
@@ -103,11 +115,96 @@ struct Shared {
     int book[KM];
     int ord[KM], state[KM];              // QP: factor order (members), bound state per member
     double w[KM], x[KM], c[KM];
+    double sinv[258];                    // 1 / n for the Welford updates (n <= 257)
+    double S[KM * (KM + 1) / 2];
     union {
         double hv[KM][65];               // staged history chunk [member][date]
-        double L[KM][KM + 1];            // Cholesky slots
+        double L[KM * (KM + 1) / 2];     // Cholesky factor of S_FF (packed by member pair)
     } u;
 };
+
+static_assert(sizeof(Shared<kMaxK>) <= 160 * 1024, "rebalance LDS over the CU's 160 KB");
+
+// Welford pairwise-complete covariance (pandas nancorr(cov=True), KKT:821-822: rows in date
+// order, a pair's rows where both values are finite) of the k members' history rows [0, rows)
+// into sh.S.  Rows are staged through LDS 64 at a time (get(m, row): value or NaN), every
+// thread issuing its loads of a chunk back to back; one thread per member pair.
+template <int KM, class Get>
+__device__ __forceinline__ void book_cov(Shared<KM>& sh, const int k, const int64_t rows,
+                                         Get get) {
+    const int tid = threadIdx.x;
+    constexpr int EPT = KM * 64 / kT;                // staged values per thread
+    for (int e = tid; e <= 257; e += kT) sh.sinv[e] = e ? 1. / (double)e : 0.0;
+    const bool table = rows <= 256;                  // nobs + 1 <= 257
+    const int npairs = k * (k + 1) / 2;
+    constexpr int P = KM >= 64 ? 4 : 1;              // member pairs per thread and pass
+    for (int pb = 0; pb < npairs; pb += P * kT) {
+        int pi[P], pj[P], nobs[P];
+        double mx[P], my[P], cxy[P], invn[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const int pq = pb + p * kT + tid;
+            int a = 0, q = pq < npairs ? pq : 0;     // pq -> (xi >= yi), row-major lower triangle
+            while (q > a) { q -= a + 1; ++a; }
+            pi[p] = a;
+            pj[p] = q;
+            nobs[p] = 0;
+            invn[p] = 1.0;
+            mx[p] = 0;
+            my[p] = 0;
+            cxy[p] = 0;
+        }
+        for (int64_t h0 = 0; h0 < rows; h0 += 64) {
+            double v[EPT];
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
+                const int e = tid + j * kT;
+                v[j] = e < k * 64 ? get(e >> 6, h0 + (e & 63)) : 0.0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < EPT; ++j) {
+                const int e = tid + j * kT;
+                if (e < k * 64) sh.u.hv[e >> 6][e & 63] = v[j];
+            }
+            __syncthreads();
+            const int nd = (int)((rows - h0) < 64 ? (rows - h0) : 64);
+            // P independent Welford chains, branch-free; 1 / (nobs + 1) comes from the table,
+            // fetched one date ahead (or divided when the window exceeds the table)
+            for (int d = 0; d < nd; ++d) {
+                double vx[P], vy[P];
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    vx[p] = sh.u.hv[pi[p]][d];
+                    vy[p] = sh.u.hv[pj[p]][d];
+                }
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const bool f = __builtin_isfinite(vx[p]) && __builtin_isfinite(vy[p]);
+                    const double inv = table ? invn[p] : 1. / (double)(nobs[p] + 1);
+                    const double dx = vx[p] - mx[p], dy = vy[p] - my[p];
+                    const double mxn = mx[p] + inv * dx;
+                    const double myn = my[p] + inv * dy;
+                    const double cn = cxy[p] + (vx[p] - mxn) * dy;
+                    nobs[p] += f ? 1 : 0;
+                    mx[p] = f ? mxn : mx[p];
+                    my[p] = f ? myn : my[p];
+                    cxy[p] = f ? cn : cxy[p];
+                    if (table) invn[p] = sh.sinv[nobs[p] + 1];
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            if (pb + p * kT + tid < npairs) {
+                double cv = __builtin_nan("");
+                if (nobs[p] >= 2) cv = cxy[p] / ((double)nobs[p] - 1.0);
+                sh.S[tri(pi[p], pj[p])] = cv;
+            }
+        }
+    }
+    __syncthreads();
+}
 
 // k largest keys among candidates (key valid when cand), ties -> smaller index first.
 // Writes the selected indices, sorted (key desc, index asc), to out[0..k).
@@ -340,59 +437,89 @@ __device__ __forceinline__ double rdlane(double v, int l) {   // l uniform
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// min w'Sw  s.t. sum w = 1, lo <= w <= hi for the n x n covariance S (global, row stride ld,
-// both triangles) -> sh.w, by the primal active-set method of oracle/portfolio.py:box_qp_weights
-// (KKT:811-833 solved exactly).  Each step solves [S_FF 1; 1' 0][w_F; lam] = [-S_FB w_B; b]
-// through a Cholesky factor of S_FF that is UPDATED, not refactored, as the free set changes:
-// a member bound by the ratio test leaves by a rank-1 update of the rows factored after it, a
-// member released by its multiplier joins as a new last row (one triangular solve).  All of it
-// runs on wave 0, lanes owning factor positions a = lane + 64 r; the sequential chains
-// (substitutions, the update sweep) broadcast one value per step with v_readlane.  Returns true
-// if the iteration cap was hit (uniform in wave 0); non-finite S -> NaN weights, capped.
+// min w'Sw  s.t. sum w = 1, lo <= w <= hi for the k x k covariance sh.S -> sh.w, by the primal
+// active-set method of oracle/portfolio.py:box_qp_weights (KKT:811-833 solved exactly).  Each
+// step solves [S_FF 1; 1' 0][w_F; lam] = [-S_FB w_B; b] with M = S_FF^-1 kept EXPLICITLY and
+// updated as the free set F changes: a member bound by the ratio test leaves by the rank-1
+// deflation M <- M - m_j m_j' / M_jj, a member released by its multiplier joins by bordering
+// (u = M s, d = S_jj - s'u, M <- M + u u'/d).  Every step is then a handful of lane-parallel
+// matrix-vector products and rank-1 updates -- no sequential substitution chain.  The optimum is
+// unique (S positive definite), so only the end point, not the path, is compared with the
+// oracle's refactor-every-step solve (rel 1e-9).
+//
+// qp_setup (every thread of the block): the start point w = 1/k, all members free, and
+// M = S^-1 by the sweep operator over all k members, each pivot's update spread over the block.
+// Returns false (uniform) when S is not finite: weights NaN, iteration cap reported.
 template <int KM>
-__device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const double* S, const int ld, const int n,
-                        const double lo, const double hi) {
-    constexpr int R = (KM + 63) / 64;
-    const int lane = threadIdx.x & 63;
-    double (*L)[KM + 1] = sh.u.L;
-    bool bad = false;
-    for (int e = lane; e < n * n; e += 64) bad |= !__builtin_isfinite(S[(e / n) * ld + e % n]);
-    if (__ballot(bad)) {
-        for (int q = lane; q < n; q += 64) sh.w[q] = __builtin_nan("");
-        lds_sync();
-        return true;
+__device__ __forceinline__ bool qp_setup(Shared<KM>& sh, const int n) {
+    const int tid = threadIdx.x;
+    const int np = n * (n + 1) / 2;
+    int bad = 0;
+    for (int e = tid; e < np; e += kT) bad |= !__builtin_isfinite(sh.S[e]);
+    if (__syncthreads_or(bad)) {
+        for (int q = tid; q < n; q += kT) sh.w[q] = __builtin_nan("");
+        __syncthreads();
+        return false;
     }
-    for (int q = lane; q < n; q += 64) {
+    for (int q = tid; q < n; q += kT) {
         sh.w[q] = 1.0 / n;
         sh.state[q] = 0;
         sh.ord[q] = q;
     }
-    for (int e = lane; e < n * n; e += 64) {
-        const int a = e / n, b = e % n;
-        if (b <= a) L[a][b] = S[a * ld + b];
+    // sweep(k): A_ij -= A_ik A_jk / A_kk (i, j != k); A_ik /= A_kk; A_kk = -1 / A_kk.  After every
+    // member is swept, A = -S^-1.  The packed elements stay in registers (EPT per thread); each
+    // pivot publishes its column through LDS (double-buffered: one barrier per pivot).
+    constexpr int EPT = (KM * (KM + 1) / 2 + kT - 1) / kT;
+    double av[EPT];
+    int ij[EPT];
+#pragma unroll
+    for (int m = 0; m < EPT; ++m) {
+        const int e = tid + m * kT;
+        int i = (int)((__builtin_sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+        if (i * (i + 1) / 2 > e) --i;
+        if ((i + 1) * (i + 2) / 2 <= e) ++i;
+        ij[m] = (i << 16) | (e - i * (i + 1) / 2);
+        av[m] = e < np ? sh.S[e] : 0.0;
     }
-    lds_sync();
-    for (int k = 0; k < n; ++k) {                      // right-looking Cholesky of S
-        const double d = __builtin_sqrt(L[k][k]);
-        lds_sync();
-        if (lane == 0) L[k][k] = d;
+    for (int k = 0; k < n; ++k) {
+        double* colk = (k & 1) ? sh.x : sh.c;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int a = lane + 64 * r;
-            if (a > k && a < n) L[a][k] = L[a][k] / d;
-        }
-        lds_sync();
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int a = lane + 64 * r;
-            if (a > k && a < n) {
-                const double lak = L[a][k];
-                for (int b = k + 1; b <= a; ++b) L[a][b] = L[a][b] - lak * L[b][k];
+        for (int m = 0; m < EPT; ++m) {
+            const int i = ij[m] >> 16, j = ij[m] & 0xffff;
+            if (tid + m * kT < np) {
+                if (j == k) colk[i] = av[m];
+                else if (i == k) colk[j] = av[m];
             }
         }
-        lds_sync();
+        __syncthreads();
+        const double rd = 1.0 / colk[k];
+#pragma unroll
+        for (int m = 0; m < EPT; ++m) {
+            const int i = ij[m] >> 16, j = ij[m] & 0xffff;
+            if (tid + m * kT < np) {
+                if (i != k && j != k) av[m] -= colk[i] * colk[j] * rd;
+                else if (i == k && j == k) av[m] = -rd;
+                else av[m] = av[m] * rd;
+            }
+        }
     }
+#pragma unroll
+    for (int m = 0; m < EPT; ++m)
+        if (tid + m * kT < np) sh.u.L[tid + m * kT] = -av[m];   // M = S^-1
+    __syncthreads();
+    return true;
+}
 
+// The iterations, on wave 0 alone (no workgroup barrier inside): lanes own free-list
+// positions a = lane + 64 r (sh.ord[a] = member).  Returns true if the iteration cap was hit
+// (uniform in wave 0).
+template <int KM>
+__device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const int n, const double lo,
+                                        const double hi) {
+    constexpr int R = (KM + 63) / 64;
+    const int lane = threadIdx.x & 63;
+    double* M = sh.u.L;
+    int* blist = sh.idxsel;                            // bound members (selection is done)
     int nf = n;
     bool capped = false;
     const int max_it = 4 * n + 8;
@@ -400,69 +527,51 @@ __device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const double* S, const i
         if (nf == 0) break;
         if (it == max_it - 1) capped = true;
         int oq[R];
-        double y1[R], y2[R];
         double bs = 0.0;
+        int nb = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int q = lane + 64 * r;
-            if (q < n && sh.state[q] != 0) bs += sh.w[q];
-            const int a = lane + 64 * r;
-            oq[r] = a < nf ? sh.ord[a] : 0;
+            const int p = lane + 64 * r;                // as a member index: bound list + sum
+            const bool isb = p < n && sh.state[p] != 0;
+            if (isb) bs += sh.w[p];
+            const u64 m = __ballot(isb);
+            if (isb) blist[nb + __popcll(m & ((1ull << lane) - 1ull))] = p;
+            nb += __popcll(m);
+            oq[r] = p < nf ? sh.ord[p] : 0;             // as a free-list position
         }
         const double bfree = 1.0 - wave_sum(bs);
+        lds_sync();
+        double cpos[R];                                // c = S_FB w_B, by free position
 #pragma unroll
-        for (int r = 0; r < R; ++r) {                  // c = S_FB w_B
+        for (int r = 0; r < R; ++r) {
             double cc = 0.0;
-            if (lane + 64 * r < nf)
-                for (int q = 0; q < n; ++q)
-                    if (sh.state[q] != 0) cc = cc + S[q * ld + oq[r]] * sh.w[q];
-            y1[r] = 1.0;
-            y2[r] = cc;
+            if (lane + 64 * r < nf) {
+#pragma unroll 4
+                for (int i = 0; i < nb; ++i) {
+                    const int q = blist[i];
+                    cc = cc + sh.S[tri(q, oq[r])] * sh.w[q];
+                }
+            }
+            cpos[r] = cc;
         }
-        // S_FF y = rhs for both right-hand sides: forward (L) then backward (L')
-        for (int b = 0; b < nf; ++b) {
-            const int rb = b >> 6, lb = b & 63;
-            const int qb = sh.ord[b];
-            const double lbb = L[qb][qb];
-            double v1 = 0.0, v2 = 0.0;
+        // y1 = M 1, y2 = M c over the free set; position b's member and c_b by v_readlane
+        double y1[R], y2[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (r == rb) {
-                    if (lane == lb) { y1[r] = y1[r] / lbb; y2[r] = y2[r] / lbb; }
-                    v1 = rdlane(y1[r], lb);
-                    v2 = rdlane(y2[r], lb);
-                }
-            }
+        for (int r = 0; r < R; ++r) { y1[r] = 0.0; y2[r] = 0.0; }
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int a = lane + 64 * r;
-                if (a > b && a < nf) {
-                    const double l = L[oq[r]][qb];
-                    y1[r] = y1[r] - l * v1;
-                    y2[r] = y2[r] - l * v2;
-                }
-            }
-        }
-        for (int a = nf - 1; a >= 0; --a) {
-            const int ra = a >> 6, la = a & 63;
-            const int qa = sh.ord[a];
-            const double laa = L[qa][qa];
-            double v1 = 0.0, v2 = 0.0;
+        for (int rb = 0; rb < R; ++rb) {
+            const int lim = nf - 64 * rb < 64 ? nf - 64 * rb : 64;
+#pragma unroll 4
+            for (int lb = 0; lb < lim; ++lb) {
+                const int qb = __builtin_amdgcn_readlane(oq[rb], lb);
+                const double cb = rdlane(cpos[rb], lb);
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (r == ra) {
-                    if (lane == la) { y1[r] = y1[r] / laa; y2[r] = y2[r] / laa; }
-                    v1 = rdlane(y1[r], la);
-                    v2 = rdlane(y2[r], la);
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int b = lane + 64 * r;
-                if (b < a) {
-                    const double l = L[qa][oq[r]];
-                    y1[r] = y1[r] - l * v1;
-                    y2[r] = y2[r] - l * v2;
+                for (int r = 0; r < R; ++r) {
+                    if (lane + 64 * r < nf) {
+                        const double mab = M[tri(oq[r], qb)];
+                        y1[r] = y1[r] + mab;
+                        y2[r] = y2[r] + mab * cb;
+                    }
                 }
             }
         }
@@ -493,7 +602,8 @@ __device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const double* S, const i
                 const int q = lane + 64 * r;
                 if (q < n && sh.state[q] != 0) {
                     double g = 0.0;
-                    for (int b = 0; b < n; ++b) g = g + S[q * ld + b] * sh.w[b];
+#pragma unroll 4
+                    for (int b = 0; b < n; ++b) g = g + sh.S[tri(q, b)] * sh.w[b];
                     g = g + lam;
                     const double v = sh.state[q] < 0 ? g : -g;
                     if (v < vmin) { vmin = v; qmin = q; }
@@ -501,41 +611,59 @@ __device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const double* S, const i
             }
             wave_argmin(vmin, qmin);
             if (!(vmin < 0.0)) break;
-            // qmin joins the free set as the last factor row: l = L^-1 S[F][qmin]
-            double l[R];
+            // bordering: u = M s (s = S[F][qmin]), d = S_jj - s'u
+            const int j = qmin;
+            double sv[R], u[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) l[r] = lane + 64 * r < nf ? S[qmin * ld + oq[r]] : 0.0;
-            for (int b = 0; b < nf; ++b) {
-                const int rb = b >> 6, lb = b & 63;
-                const int qb = sh.ord[b];
-                const double lbb = L[qb][qb];
-                double v = 0.0;
+            for (int r = 0; r < R; ++r) {
+                sv[r] = lane + 64 * r < nf ? sh.S[tri(oq[r], j)] : 0.0;
+                u[r] = 0.0;
+            }
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (r == rb) {
-                        if (lane == lb) l[r] = l[r] / lbb;
-                        v = rdlane(l[r], lb);
-                    }
-                }
+            for (int rb = 0; rb < R; ++rb) {
+                const int lim = nf - 64 * rb < 64 ? nf - 64 * rb : 64;
+#pragma unroll 4
+                for (int lb = 0; lb < lim; ++lb) {
+                    const int qb = __builtin_amdgcn_readlane(oq[rb], lb);
+                    const double sb = rdlane(sv[rb], lb);
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int a = lane + 64 * r;
-                    if (a > b && a < nf) l[r] = l[r] - L[oq[r]][qb] * v;
+                    for (int r = 0; r < R; ++r)
+                        if (lane + 64 * r < nf) u[r] = u[r] + M[tri(oq[r], qb)] * sb;
                 }
             }
-            double ss = 0.0;
+            double su = 0.0;
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                if (lane + 64 * r < nf) {
-                    L[qmin][oq[r]] = l[r];
-                    ss += l[r] * l[r];
+                if (lane + 64 * r < nf) su += sv[r] * u[r];
+            const double d = sh.S[tri(j, j)] - wave_sum(su);
+            const double rd = 1.0 / d;
+            double ua[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) ua[r] = u[r] * rd;
+#pragma unroll
+            for (int rb = 0; rb < R; ++rb) {
+                const int lim = nf - 64 * rb < 64 ? nf - 64 * rb : 64;
+#pragma unroll 4
+                for (int lb = 0; lb < lim; ++lb) {
+                    const int b = 64 * rb + lb;
+                    const int qb = __builtin_amdgcn_readlane(oq[rb], lb);
+                    const double ub = rdlane(u[rb], lb);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        if (lane + 64 * r < nf && lane + 64 * r >= b) {
+                            const int e = tri(oq[r], qb);
+                            M[e] = M[e] + ua[r] * ub;
+                        }
+                    }
                 }
-            ss = wave_sum(ss);
-            lds_sync();
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (lane + 64 * r < nf) M[tri(oq[r], j)] = -ua[r];
             if (lane == 0) {
-                L[qmin][qmin] = __builtin_sqrt(S[qmin * ld + qmin] - ss);
-                sh.ord[nf] = qmin;
-                sh.state[qmin] = 0;
+                M[tri(j, j)] = rd;
+                sh.ord[nf] = j;
+                sh.state[j] = 0;
             }
             lds_sync();
             ++nf;
@@ -580,51 +708,40 @@ __device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const double* S, const i
                     sh.w[jb] = (code & 1) ? hi : lo;
                     sh.state[jb] = (code & 1) ? 1 : -1;
                 }
-                // factor position of jb; rows after it absorb its column (rank-1 update)
-                int j = 0;
+                // deflation M <- M - m m' / m_jj over F \ {jb}, m = M[F][jb]
+                int pj = 0;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const u64 m = __ballot(lane + 64 * r < nf && oq[r] == jb);
-                    if (m) j = 64 * r + __builtin_ctzll(m);
+                    if (m) pj = 64 * r + __builtin_ctzll(m);
                 }
-                double xv[R];
+                const double rjj = 1.0 / M[tri(jb, jb)];
+                double mj[R], ma[R];
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const int a = lane + 64 * r;
-                    xv[r] = (a > j && a < nf) ? L[oq[r]][jb] : 0.0;
+                    mj[r] = lane + 64 * r < nf ? M[tri(oq[r], jb)] : 0.0;
+                    ma[r] = mj[r] * rjj;
                 }
-                for (int k = j + 1; k < nf; ++k) {
-                    const int rk = k >> 6, lk = k & 63;
-                    const int qk = sh.ord[k];
-                    const double lkk = L[qk][qk];
-                    double xk = 0.0;
 #pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        if (r == rk) xk = rdlane(xv[r], lk);
-                    const double rr = __builtin_sqrt(lkk * lkk + xk * xk);
-                    const double cs = rr / lkk, sn = xk / lkk;
-                    lds_sync();
-                    if (lane == 0) L[qk][qk] = rr;
+                for (int rb = 0; rb < R; ++rb) {
+                    const int lim = nf - 64 * rb < 64 ? nf - 64 * rb : 64;
+#pragma unroll 4
+                    for (int lb = 0; lb < lim; ++lb) {
+                        const int b = 64 * rb + lb;
+                        const int qb = __builtin_amdgcn_readlane(oq[rb], lb);
+                        const double mb = rdlane(mj[rb], lb);
 #pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const int a = lane + 64 * r;
-                        if (a > k && a < nf) {
-                            const double ln = (L[oq[r]][qk] + sn * xv[r]) / cs;
-                            L[oq[r]][qk] = ln;
-                            xv[r] = cs * xv[r] - sn * ln;
+                        for (int r = 0; r < R; ++r) {
+                            const int a = lane + 64 * r;
+                            if (a < nf && a >= b && a != pj && b != pj) {
+                                const int e = tri(oq[r], qb);
+                                M[e] = M[e] - ma[r] * mb;
+                            }
                         }
                     }
                 }
-                int nxt[R];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const int a = lane + 64 * r;
-                    nxt[r] = (a >= j && a + 1 < nf) ? sh.ord[a + 1] : -1;
-                }
                 lds_sync();
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (nxt[r] >= 0) sh.ord[lane + 64 * r] = nxt[r];
+                if (lane == 0) sh.ord[pj] = sh.ord[nf - 1];  // the last position fills the gap
                 lds_sync();
                 --nf;
             }
@@ -634,68 +751,28 @@ __device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const double* S, const i
     return capped;
 }
 
-// Welford pairwise-complete covariance (pandas nancorr, cov=True) of a dense [rows][ld] matrix
-// (k columns, NaN = missing) into S [k][k]; rows staged 64 at a time.
-template <int KM>
-__device__ __forceinline__ void dense_cov(Shared<KM>& sh, const double* R, int64_t rows, int64_t ld, int k,
-                          double* S) {
-    const int tid = threadIdx.x;
-    const int npairs = k * (k + 1) / 2;
-    for (int pb = 0; pb < npairs; pb += kT) {
-        const int pq = pb + tid;
-        int pi = 0, pj = 0;
-        if (pq < npairs) {
-            int q = pq;
-            while (q > pi) { q -= pi + 1; ++pi; }
-            pj = q;
-        }
-        double nobs = 0, mx = 0, my = 0, cxy = 0;
-        for (int64_t h0 = 0; h0 < rows; h0 += 64) {
-            __syncthreads();
-            for (int e = tid; e < k * 64; e += kT) {
-                const int m = e / 64, d = e % 64;
-                sh.u.hv[m][d] = (h0 + d < rows) ? R[(h0 + d) * ld + m] : __builtin_nan("");
-            }
-            __syncthreads();
-            if (pq < npairs) {
-                const int nd = (int)((rows - h0) < 64 ? (rows - h0) : 64);
-                for (int d = 0; d < nd; ++d) {
-                    const double vx = sh.u.hv[pi][d], vy = sh.u.hv[pj][d];
-                    if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
-                        nobs += 1;
-                        const double dx = vx - mx, dy = vy - my;
-                        mx += 1. / nobs * dx;
-                        my += 1. / nobs * dy;
-                        cxy += (vx - mx) * dy;
-                    }
-                }
-            }
-        }
-        if (pq < npairs) {
-            double cv = __builtin_nan("");
-            if (nobs >= 1 && (nobs - 1.0) != 0) cv = cxy / (nobs - 1.0);
-            S[pi * k + pj] = cv;
-            S[pj * k + pi] = cv;
-        }
-    }
-    __syncthreads();
-}
 
-// determine_weights for one book: covariance into `cov` (an output), then the QP reading it
+// determine_weights for one book: [rows][ld] returns (k columns, NaN = missing) -> covariance
+// (an output) and weights
 __global__ __launch_bounds__(kT) void weights_kernel(const double* R, int64_t rows, int64_t ld,
                                                      int k, double lo, double hi, double* w,
                                                      double* cov, int32_t* status) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     Shared<kMaxK>& sh = *reinterpret_cast<Shared<kMaxK>*>(smem_raw);
-    dense_cov(sh, R, rows, ld, k, cov);
+    book_cov(sh, k, rows, [&](int m, int64_t row) -> double {
+        return row < rows ? R[row * ld + m] : __builtin_nan("");
+    });
     const int tid = threadIdx.x;
+    for (int e = tid; e < k * k; e += kT) cov[e] = sh.S[tri(e / k, e % k)];
     bool capped = false;
     if (k * hi <= 1.0) {
         if (tid < k) sh.w[tid] = hi;
     } else if (k * lo >= 1.0) {
         if (tid < k) sh.w[tid] = lo;
+    } else if (!qp_setup(sh, k)) {
+        capped = true;
     } else if (tid < 64) {
-        capped = qp_wave(sh, cov, k, k, lo, hi);
+        capped = qp_wave(sh, k, lo, hi);
     }
     __syncthreads();
     if (tid < k) w[tid] = sh.w[tid];
@@ -767,6 +844,7 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
     }
     if (tid == 0 && side == 0) r.k_out[i] = k;
 
+    if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 0] = wall_clock64();
     const bool largest = side == 0;
     if (k > 0 && regk) {
         if (!select_top_reg<KR>(sh, ks, k, largest, sh.book))
@@ -778,65 +856,71 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
 
     const int64_t hlo = r.window > 0 ? (t - r.window > 0 ? t - r.window : 0) : r.h_t0;
     const int64_t hhi = r.window > 0 ? t : r.h_t1;
+    if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 1] = wall_clock64();
     const int* bk = sh.book;
-    double* S = r.cov + (i * 2 + side) * (int64_t)r.top_n * r.top_n;
-    // ---- pairwise-complete covariance (pandas nancorr, cov=True), into the scratch S ----------
-    const int npairs = k * (k + 1) / 2;
-    for (int pb = 0; pb < npairs; pb += kT) {
-        const int pq = pb + tid;
-        int pi = 0, pj = 0;
-        if (pq < npairs) {   // pq -> (xi >= yi) in row-major lower-triangle order
-            int q = pq;
-            pi = 0;
-            while (q > pi) { q -= pi + 1; ++pi; }
-            pj = q;
+    // ---- pairwise-complete covariance of the book's history window ------------------------
+    const int64_t rows = hhi - hlo;
+    auto gather = [&](int m, int64_t row) -> double {
+        const int64_t th = hlo + row;
+        const int64_t tt = th < hhi ? th : hlo;              // loads always in bounds
+        const int a = bk[m];
+        const u64 wb = r.hbits[(tt >> 6) * r.lda + a];
+        const double hv = r.hist[tt * r.lda + a];
+        return (th < hhi && ((wb >> (tt & 63)) & 1ull)) ? hv : __builtin_nan("");
+    };
+    if (r.probe & 2) {
+        for (int e = tid; e < k * (k + 1) / 2; e += kT) {
+            int a = 0, q = e;
+            while (q > a) { q -= a + 1; ++a; }
+            sh.S[e] = a == q ? 1e-4 : 1e-6;
         }
-        double nobs = 0, mx = 0, my = 0, cxy = 0;
-        for (int64_t h0 = hlo; h0 < hhi; h0 += 64) {
-            __syncthreads();
-            for (int e = tid; e < k * 64; e += kT) {
-                int m = e / 64, d = e % 64;
-                int64_t th = h0 + d;
-                double v = __builtin_nan("");
-                if (th < hhi && bit_at(r.hbits, r.lda, th, bk[m])) v = r.hist[th * r.lda + bk[m]];
-                sh.u.hv[m][d] = v;
+        __syncthreads();
+    } else if (k * (k + 1) / 2 <= kT || r.hscr == nullptr) {
+        book_cov(sh, k, rows, gather);                      // one pass over the member pairs
+    } else {
+        // several passes: gather the members' window once into a contiguous [member][row]
+        // scratch block, which every pass then stages with coalesced reads
+        double* H = r.hscr + (i * 2 + side) * (int64_t)r.top_n * r.hrows;
+        const int64_t ne = (int64_t)k * rows;
+        for (int64_t e0 = 0; e0 < ne; e0 += 4 * kT) {
+            double v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t e = e0 + j * kT + tid;
+                v[j] = e < ne ? gather((int)(e / rows), e % rows) : 0.0;
             }
-            __syncthreads();
-            if (pq < npairs) {
-                const int nd = (int)((hhi - h0) < 64 ? (hhi - h0) : 64);
-                for (int d = 0; d < nd; ++d) {
-                    double vx = sh.u.hv[pi][d], vy = sh.u.hv[pj][d];
-                    if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
-                        nobs += 1;
-                        double dx = vx - mx, dy = vy - my;
-                        mx += 1. / nobs * dx;
-                        my += 1. / nobs * dy;
-                        cxy += (vx - mx) * dy;
-                    }
-                }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t e = e0 + j * kT + tid;
+                if (e < ne) H[e] = v[j];
             }
         }
-        if (pq < npairs) {
-            double cv = __builtin_nan("");
-            if (nobs >= 1 && (nobs - 1.0) != 0) cv = cxy / (nobs - 1.0);
-            S[pi * k + pj] = cv;
-            S[pj * k + pi] = cv;
-        }
+        __syncthreads();
+        if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 5] = wall_clock64();
+        book_cov(sh, k, rows, [&](int m, int64_t row) -> double {
+            return row < rows ? H[m * rows + row] : __builtin_nan("");
+        });
     }
-    __syncthreads();
 
     // ---- exact box-constrained QP (primal active set, wave 0) -----------------------------
+    if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 2] = wall_clock64();
     bool capped = false;
     if (k > 0 && k * r.hi <= 1.0) {
         if (tid < k) sh.w[tid] = r.hi;
     } else if (k > 0 && k * r.lo >= 1.0) {
         if (tid < k) sh.w[tid] = r.lo;
-    } else if (k > 0 && tid < 64) {
-        capped = qp_wave(sh, S, k, k, r.lo, r.hi);
+    } else if (k > 0 && (r.probe & 1)) {
+        if (tid < k) sh.w[tid] = 1.0 / k;
+    } else if (k > 0) {
+        const bool ok = qp_setup(sh, k);
+        if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 6] = wall_clock64();
+        if (!ok) capped = true;
+        else if (tid < 64) capped = qp_wave(sh, k, r.lo, r.hi);
     }
     if (capped && tid == 0) atomicOr(&r.status[i], 1);
     __syncthreads();
     // ---- outputs for this book -----------------------------------------------------------
+    if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 3] = wall_clock64();
     double* wout = r.weights + (i * 2 + side) * kMaxK;
     int32_t* bout = r.books + (i * 2 + side) * kMaxK;
     if (tid < k) {
@@ -870,6 +954,7 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
             r.upos[((i * 2 + side) * 2 + q) * kMaxK + tid] = pos;
         }
     }
+    if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 4] = wall_clock64();
     if (side == 0 && tid < 2) {
         const int other = tid == 0 ? 0 : 2;
         int64_t tot = 0;
@@ -1274,14 +1359,38 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
                       books && weights && sums && upos && usize && status, "null buffer");
     AFM_CHECK_ARG(lo <= hi, "lo > hi");
     if (nd <= 0) return AFM_OK;
-    double* cov = nullptr;
-    const size_t b_cov = sizeof(double) * (size_t)nd * 2 * ((size_t)top_n * top_n + 1);
-    AFM_HIP(hipMallocAsync((void**)&cov, b_cov, ctx->stream));
     AFM_HIP(hipMemsetAsync(status, 0, sizeof(int32_t) * (size_t)nd, ctx->stream));
+    // books of more than one pass of member pairs re-stage their history once per pass: give
+    // them a contiguous copy of their window
+    const int64_t hrows = window > 0 ? window : (h_t1 > h_t0 ? h_t1 - h_t0 : 0);
+    double* hscr = nullptr;
+    if (top_n * (top_n + 1) / 2 > kT && hrows > 0)
+        AFM_HIP(hipMallocAsync((void**)&hscr, sizeof(double) * (size_t)nd * 2 * top_n * hrows,
+                               ctx->stream));
     RebArgs r{T, lda, A, dates, nd, pred, trad_bits, hist, hist_bits, h_t0, h_t1, window, close,
-              tmr, top_n, lo, hi, cov, k_out, books, weights, sums, upos, usize, status};
+              tmr, top_n, lo, hi, hscr, hrows, 0, nullptr, k_out, books, weights, sums, upos, usize, status};
+    if (const char* e = getenv("AFM_REB_PROBE")) r.probe = atoi(e);
+    if (r.probe & 4) AFM_HIP(hipMallocAsync((void**)&r.stamps, sizeof(int64_t) * nd * 16, ctx->stream));
     const int rc = top_n <= 32 ? launch_rebalance<32>(ctx, r) : launch_rebalance<kMaxK>(ctx, r);
-    AFM_HIP(hipFreeAsync(cov, ctx->stream));
+    if (r.stamps) {                  // experiment: mean phase durations per workgroup
+        std::vector<int64_t> h((size_t)nd * 16);
+        AFM_HIP(hipMemcpyAsync(h.data(), r.stamps, sizeof(int64_t) * nd * 16, hipMemcpyDeviceToHost,
+                               ctx->stream));
+        AFM_HIP(hipStreamSynchronize(ctx->stream));
+        double acc[6] = {0, 0, 0, 0, 0, 0};
+        for (int64_t b = 0; b < nd * 2; ++b) {
+            const int64_t* x = &h[b * 8];
+            for (int j = 0; j < 4; ++j) acc[j] += (double)(x[j + 1] - x[j]);
+            acc[4] += (double)(x[5] - x[1]);
+            acc[5] += (double)(x[6] - x[2]);
+        }
+        const double f = 1.0 / (nd * 2 * 100.0);
+        fprintf(stderr, "rebalance phases (us/workgroup, 100 MHz clock): select %.1f cov %.1f "
+                "(gather %.1f) qp %.1f (setup %.1f) out %.1f\n", acc[0] * f, acc[1] * f, acc[4] * f,
+                acc[2] * f, acc[5] * f, acc[3] * f);
+        AFM_HIP(hipFree(r.stamps));
+    }
+    if (hscr) AFM_HIP(hipFreeAsync(hscr, ctx->stream));
     return rc;
 }
 

@@ -4,7 +4,8 @@
 Corrections (MI355X_MICROARCH.md, HBM section): both counters are in KiB; on gfx950 FETCH_SIZE
 reports half the bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is taken
 as is.  Output: JSON {kernel: {"fetch_bytes", "write_bytes", "hbm_bytes", "launches"}} per
-launch (averaged over the launches of the profiled command).
+launch (averaged over the launches of the profiled command), keyed by kernel name and by
+kernel name + template arguments.
 
 Usage: tools/pmc_traffic.py <pmc dir (with fetch/ and write/)> <out.json> [assets days]
 (the bench workload the passes profiled; default 10000 5040)
@@ -14,10 +15,19 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import short  # noqa: E402
+
+
+def templated(name):
+    """short() plus the template arguments: zgram_kernel<7, 1, true> and zgram_kernel<2, 0,
+    false> are different kernels with different traffic."""
+    k = short(name)
+    m = re.search(re.escape(k) + r"(<[^()]*?>)\(", name)
+    return k + m.group(1) if m else k
 
 
 def per_launch(path, counter):
@@ -27,9 +37,9 @@ def per_launch(path, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            k = short(r["Kernel_Name"])
-            tot[k] += float(r["Counter_Value"])
-            disp[k].add(r["Dispatch_Id"])
+            for k in {short(r["Kernel_Name"]), templated(r["Kernel_Name"])}:
+                tot[k] += float(r["Counter_Value"])
+                disp[k].add(r["Dispatch_Id"])
     return {k: (tot[k] / len(disp[k]), len(disp[k])) for k in tot}
 
 
