@@ -182,61 +182,212 @@ struct PrepArgs {
     int32_t* nrows;           // [T] surviving rows per date
 };
 
-__global__ __launch_bounds__(kWT) void xs_prepare_kernel(PrepArgs g) {
-    __shared__ PwShared pw;
-    __shared__ int sbuf[kWT / 64];
-    const int tid = threadIdx.x;
+constexpr int kPT = 256;               // xs_prepare threads (4 waves)
+constexpr int kMaxWords = 1024;        // A <= 65536
+constexpr int kPwStack = 16;           // pairwise-tree depth bound (n <= 65536: <= 10 levels)
+
+struct PrepShared {
+    u64 mw[3][kMaxWords];              // row masks per step k: signal and returns 1..k present
+    int pre[3][kMaxWords + 1];         // exclusive prefix counts of the mask words
+    int loff[3][kMaxLeaves / 2], llen[3][kMaxLeaves / 2];
+    double lval[3][kMaxLeaves / 2];
+    int nleaf[3];
+    double mu[3];
+};
+
+// numpy pairwise leaves of n values (the pw_enum recursion, iteratively): (offset, length <= 128)
+// in left-to-right order
+__device__ int pw_leaves(int n, int* loff, int* llen) {
+    int so[kPwStack], sn[kPwStack], top = 0, nl = 0;
+    so[0] = 0;
+    sn[0] = n;
+    while (top >= 0) {
+        const int off = so[top], m = sn[top];
+        --top;
+        if (m <= 128) {
+            loff[nl] = off;
+            llen[nl] = m;
+            ++nl;
+        } else {
+            int m2 = m / 2;
+            m2 -= m2 % 8;
+            so[top + 1] = off + m2; sn[top + 1] = m - m2;     // right, popped second
+            so[top + 2] = off;      sn[top + 2] = m2;         // left, popped first
+            top += 2;
+        }
+    }
+    return nl;
+}
+
+// the pw_combine recursion over the leaf sums, iteratively: post-order with an explicit stack
+__device__ double pw_tree(int n, const double* lval) {
+    int sm[kPwStack], st[kPwStack];
+    double sl[kPwStack];
+    int top = 0, cursor = 0;
+    sm[0] = n;
+    st[0] = 0;
+    double val = 0.0;
+    bool up = false;                                   // val holds a finished subtree sum
+    for (;;) {
+        if (up) {
+            if (top < 0) return val;
+            if (st[top] == 1) {                        // left child done: descend right
+                sl[top] = val;
+                st[top] = 2;
+                int m2 = sm[top] / 2;
+                m2 -= m2 % 8;
+                ++top;
+                sm[top] = sm[top - 1] - m2;
+                st[top] = 0;
+                up = false;
+            } else {                                   // right child done
+                val = sl[top] + val;
+                --top;
+            }
+            continue;
+        }
+        const int m = sm[top];
+        if (m <= 128) {
+            val = lval[cursor++];
+            --top;
+            up = true;
+        } else {
+            st[top] = 1;
+            int m2 = m / 2;
+            m2 -= m2 % 8;
+            ++top;
+            sm[top] = m2;
+            st[top] = 0;
+        }
+    }
+}
+
+// One workgroup (4 waves) per date.  The three row masks (KKT:313 merge + dropna steps) as bit
+// words by ballot over coalesced 64-asset segments; their prefix counts; every numpy pairwise
+// leaf of the three compacted return columns summed by its own thread (8 accumulators fed by
+// groups of 8 independent loads, the leaf's rows found from the mask words); the tree of leaf
+// sums in numpy's order; then the surviving rows written compacted with demeaned returns.
+__global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
+    __shared__ PrepShared sh;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t t = blockIdx.x;
     const int64_t plane = g.T * g.lda;
     const double* sig = g.sig + t * g.lda;
-    double* scr = g.scratch + t * g.lda;
-    double mu[3];
-    for (int k = 0; k < 3; ++k) {
-        // rows surviving step k: signal and returns 1..k all present
-        int n = 0;
-        for (int64_t base = 0; base < g.A; base += kWT) {
-            const int64_t a = base + tid;
-            int ok = 0;
-            double v = 0.0;
-            if (a < g.A) {
-                ok = sig[a] == sig[a];
-                for (int q = 0; q <= k && ok; ++q) {
-                    double r = g.fr[q * plane + t * g.lda + a];
-                    ok = r == r;
-                }
-                v = g.fr[k * plane + t * g.lda + a];
-            }
-            int ex;
-            const int tot = block_scan<kWT>(ok, sbuf, &ex);
-            if (ok) scr[n + ex] = v;
-            n += tot;
+    const double* fr0 = g.fr + t * g.lda;
+    const int nw = (int)((g.A + 63) / 64);
+    // ---- masks ---------------------------------------------------------------------------
+    for (int w0 = wave; w0 < nw; w0 += 16) {
+        double v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t a = (int64_t)(w0 + 4 * u) * 64 + lane;
+            const bool in = w0 + 4 * u < nw && a < g.A;
+            v[u][0] = in ? sig[a] : qnan();
+#pragma unroll
+            for (int q = 0; q < 3; ++q) v[u][1 + q] = in ? fr0[q * plane + a] : qnan();
         }
-        __syncthreads();
-        mu[k] = n > 0 ? block_np_sum<kWT>(pw, scr, n) / (double)n : qnan();
-    }
-    // final rows (all three returns), compacted with demeaned returns
-    int n = 0;
-    for (int64_t base = 0; base < g.A; base += kWT) {
-        const int64_t a = base + tid;
-        int ok = 0;
-        if (a < g.A) {
-            ok = sig[a] == sig[a];
-            for (int q = 0; q < 3 && ok; ++q) {
-                double r = g.fr[q * plane + t * g.lda + a];
-                ok = r == r;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int w = w0 + 4 * u;
+            bool ok = v[u][0] == v[u][0];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                ok = ok && v[u][1 + q] == v[u][1 + q];
+                const u64 m = __ballot(ok);
+                if (lane == 0 && w < nw) sh.mw[q][w] = m;
             }
         }
-        int ex;
-        const int tot = block_scan<kWT>(ok, sbuf, &ex);
-        if (ok) {
-            const int64_t o = t * g.lda + n + ex;
-            g.rows[o] = sig[a];
-            for (int q = 0; q < 3; ++q) g.rows[(1 + q) * plane + o] = g.fr[q * plane + t * g.lda + a] - mu[q];
-            g.rows_idx[o] = (int32_t)a;
-        }
-        n += tot;
     }
-    if (tid == 0) g.nrows[t] = n;
+    __syncthreads();
+    // ---- prefix counts (wave q scans mask q) -----------------------------------------------
+    if (wave < 3) {
+        int carry = 0;
+        for (int w0 = 0; w0 < nw; w0 += 64) {
+            const int w = w0 + lane;
+            const int c = w < nw ? __popcll(sh.mw[wave][w]) : 0;
+            int incl = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int x = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += x;
+            }
+            if (w < nw) sh.pre[wave][w] = carry + incl - c;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) {
+            sh.pre[wave][nw] = carry;
+            sh.nleaf[wave] = carry > 0 ? pw_leaves(carry, sh.loff[wave], sh.llen[wave]) : 0;
+        }
+    }
+    __syncthreads();
+    // ---- leaf sums: one thread per (mask, leaf) ------------------------------------------------
+    const int nl0 = sh.nleaf[0], nl1 = sh.nleaf[1], nl2 = sh.nleaf[2];
+    for (int job = tid; job < nl0 + nl1 + nl2; job += kPT) {
+        const int q = job < nl0 ? 0 : (job < nl0 + nl1 ? 1 : 2);
+        const int l = job - (q == 0 ? 0 : (q == 1 ? nl0 : nl0 + nl1));
+        const int off = sh.loff[q][l], len = sh.llen[q][l];
+        const double* x = fr0 + q * plane;
+        // first row of the leaf: the word holding compacted position off, then its bit
+        int lo = 0, hi = nw;                           // last word with pre <= off
+        while (hi - lo > 1) {
+            const int m = (lo + hi) >> 1;
+            if (sh.pre[q][m] <= off) lo = m; else hi = m;
+        }
+        int w = lo;
+        u64 rest = sh.mw[q][w];
+        for (int s = off - sh.pre[q][w]; s > 0; --s) rest &= rest - 1;
+        auto next = [&]() -> int64_t {                 // asset of the next compacted row
+            while (rest == 0ull) rest = sh.mw[q][++w];
+            const int64_t a = (int64_t)w * 64 + __builtin_ctzll(rest);
+            rest &= rest - 1;
+            return a;
+        };
+        double res;
+        if (len < 8) {
+            res = 0.;
+            for (int i = 0; i < len; ++i) res += x[next()];
+        } else {
+            double r[8];
+            int64_t ix[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ix[j] = next();
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] = x[ix[j]];
+            int i;
+            for (i = 8; i < len - (len % 8); i += 8) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ix[j] = next();
+                double v8[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v8[j] = x[ix[j]];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) r[j] += v8[j];
+            }
+            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            for (; i < len; ++i) res += x[next()];
+        }
+        sh.lval[q][l] = res;
+    }
+    __syncthreads();
+    if (tid < 3) {
+        const int n = sh.pre[tid][nw];
+        sh.mu[tid] = n > 0 ? (0.0 + pw_tree(n, sh.lval[tid])) / (double)n : qnan();
+    }
+    __syncthreads();
+    // ---- surviving rows (all three returns), compacted, returns demeaned ----------------------
+    const double mu0 = sh.mu[0], mu1 = sh.mu[1], mu2 = sh.mu[2];
+    for (int w = wave; w < nw; w += 4) {
+        const u64 m = sh.mw[2][w];
+        if (!((m >> lane) & 1ull)) continue;
+        const int64_t a = (int64_t)w * 64 + lane;
+        const int pos = sh.pre[2][w] + __popcll(m & ((1ull << lane) - 1ull));
+        const int64_t o = t * g.lda + pos;
+        g.rows[o] = sig[a];
+        g.rows[plane + o] = fr0[a] - mu0;
+        g.rows[2 * plane + o] = fr0[plane + a] - mu1;
+        g.rows[3 * plane + o] = fr0[2 * plane + a] - mu2;
+        g.rows_idx[o] = (int32_t)a;
+    }
+    if (tid == 0) g.nrows[t] = sh.pre[2][nw];
 }
 
 // ---- A3/A4: exact ranks -------------------------------------------------------------------
@@ -651,7 +802,7 @@ extern "C" int afm_xs_prepare_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t ld
     AFM_CHECK_ARG(T > 0 && A > 0 && lda >= A && lda % 64 == 0 && A <= 65536, "bad shape");
     AFM_CHECK_ARG(sig && fr && scratch && rows && rows_idx && nrows, "null buffer");
     PrepArgs g{T, lda, A, sig, fr, scratch, rows, rows_idx, nrows};
-    hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)T), dim3(kWT), 0, ctx->stream, g);
+    hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)T), dim3(kPT), 0, ctx->stream, g);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
