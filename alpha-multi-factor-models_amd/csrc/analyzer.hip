@@ -21,6 +21,7 @@
 #include "afm_internal.h"
 
 #include <algorithm>
+#include <vector>
 
 #pragma clang fp contract(off)
 
@@ -180,93 +181,33 @@ struct PrepArgs {
     double* rows;             // [4][T][lda]: factor, r1, r2, r5 of surviving rows, compacted
     int32_t* rows_idx;        // [T][lda] asset index of each compacted row
     int32_t* nrows;           // [T] surviving rows per date
+    int64_t* stamps;          // experiment (AFM_AN_PROBE): 5 phase timestamps per date, or null
+    int64_t* clk;             // experiment: shader-clock stamps at phases 0 and 4
 };
 
 constexpr int kPT = 256;               // xs_prepare threads (4 waves)
-constexpr int kMaxWords = 1024;        // A <= 65536
-constexpr int kPwStack = 16;           // pairwise-tree depth bound (n <= 65536: <= 10 levels)
+constexpr int kMaxWords = 512;         // A <= 32768
+constexpr int kMaxNodes = 1216;        // numpy pairwise-tree nodes of n <= 32768 (leaves >= 57)
+constexpr int kMaxLevels = 16;
 
 struct PrepShared {
     u64 mw[3][kMaxWords];              // row masks per step k: signal and returns 1..k present
     int pre[3][kMaxWords + 1];         // exclusive prefix counts of the mask words
-    int loff[3][kMaxLeaves / 2], llen[3][kMaxLeaves / 2];
-    double lval[3][kMaxLeaves / 2];
-    int nleaf[3];
+    int noff[kMaxNodes], nlen[kMaxNodes], nchild[kMaxNodes];   // one column's tree, level order
+    double nval[kMaxNodes];
+    int lvl[kMaxLevels + 1];           // level boundaries in the node arrays
+    int scan[kPT / 64];
     double mu[3];
 };
 
-// numpy pairwise leaves of n values (the pw_enum recursion, iteratively): (offset, length <= 128)
-// in left-to-right order
-__device__ int pw_leaves(int n, int* loff, int* llen) {
-    int so[kPwStack], sn[kPwStack], top = 0, nl = 0;
-    so[0] = 0;
-    sn[0] = n;
-    while (top >= 0) {
-        const int off = so[top], m = sn[top];
-        --top;
-        if (m <= 128) {
-            loff[nl] = off;
-            llen[nl] = m;
-            ++nl;
-        } else {
-            int m2 = m / 2;
-            m2 -= m2 % 8;
-            so[top + 1] = off + m2; sn[top + 1] = m - m2;     // right, popped second
-            so[top + 2] = off;      sn[top + 2] = m2;         // left, popped first
-            top += 2;
-        }
-    }
-    return nl;
-}
-
-// the pw_combine recursion over the leaf sums, iteratively: post-order with an explicit stack
-__device__ double pw_tree(int n, const double* lval) {
-    int sm[kPwStack], st[kPwStack];
-    double sl[kPwStack];
-    int top = 0, cursor = 0;
-    sm[0] = n;
-    st[0] = 0;
-    double val = 0.0;
-    bool up = false;                                   // val holds a finished subtree sum
-    for (;;) {
-        if (up) {
-            if (top < 0) return val;
-            if (st[top] == 1) {                        // left child done: descend right
-                sl[top] = val;
-                st[top] = 2;
-                int m2 = sm[top] / 2;
-                m2 -= m2 % 8;
-                ++top;
-                sm[top] = sm[top - 1] - m2;
-                st[top] = 0;
-                up = false;
-            } else {                                   // right child done
-                val = sl[top] + val;
-                --top;
-            }
-            continue;
-        }
-        const int m = sm[top];
-        if (m <= 128) {
-            val = lval[cursor++];
-            --top;
-            up = true;
-        } else {
-            st[top] = 1;
-            int m2 = m / 2;
-            m2 -= m2 % 8;
-            ++top;
-            sm[top] = m2;
-            st[top] = 0;
-        }
-    }
-}
-
-// One workgroup (4 waves) per date.  The three row masks (KKT:313 merge + dropna steps) as bit
-// words by ballot over coalesced 64-asset segments; their prefix counts; every numpy pairwise
-// leaf of the three compacted return columns summed by its own thread (8 accumulators fed by
-// groups of 8 independent loads, the leaf's rows found from the mask words); the tree of leaf
-// sums in numpy's order; then the surviving rows written compacted with demeaned returns.
+// One workgroup (4 waves) per date.  The three row masks of KKT:313's merge + dropna steps as
+// bit words by ballot over coalesced 64-asset segments, and their prefix counts.  Then per
+// return column: its rows compacted (ascending security id) into the scratch row, numpy's
+// pairwise summation tree of that length built level by level (node m > 128 splits at
+// m/2 - (m/2)%8, as in numpy's pairwise_sum), every leaf summed by its own thread (the
+// 8-accumulator block, or the plain loop under 8), the internal nodes added bottom-up level by
+// level: mean = (0.0 + sum) / n bit-exactly, with no serial walk of the tree.  Finally the rows
+// surviving all three steps are written compacted with demeaned returns.
 __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
     __shared__ PrepShared sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -274,7 +215,9 @@ __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
     const int64_t plane = g.T * g.lda;
     const double* sig = g.sig + t * g.lda;
     const double* fr0 = g.fr + t * g.lda;
+    double* scr = g.scratch + t * g.lda;
     const int nw = (int)((g.A + 63) / 64);
+    if (g.stamps && tid == 0) { g.stamps[t * 5 + 0] = wall_clock64(); g.clk[t * 2] = clock64(); }
     // ---- masks ---------------------------------------------------------------------------
     for (int w0 = wave; w0 < nw; w0 += 16) {
         double v[4][4];
@@ -299,6 +242,7 @@ __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
         }
     }
     __syncthreads();
+    if (g.stamps && tid == 0) g.stamps[t * 5 + 1] = wall_clock64();
     // ---- prefix counts (wave q scans mask q) -----------------------------------------------
     if (wave < 3) {
         int carry = 0;
@@ -313,66 +257,89 @@ __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
             if (w < nw) sh.pre[wave][w] = carry + incl - c;
             carry += __shfl(incl, 63, 64);
         }
-        if (lane == 0) {
-            sh.pre[wave][nw] = carry;
-            sh.nleaf[wave] = carry > 0 ? pw_leaves(carry, sh.loff[wave], sh.llen[wave]) : 0;
-        }
+        if (lane == 0) sh.pre[wave][nw] = carry;
     }
     __syncthreads();
-    // ---- leaf sums: one thread per (mask, leaf) ------------------------------------------------
-    const int nl0 = sh.nleaf[0], nl1 = sh.nleaf[1], nl2 = sh.nleaf[2];
-    for (int job = tid; job < nl0 + nl1 + nl2; job += kPT) {
-        const int q = job < nl0 ? 0 : (job < nl0 + nl1 ? 1 : 2);
-        const int l = job - (q == 0 ? 0 : (q == 1 ? nl0 : nl0 + nl1));
-        const int off = sh.loff[q][l], len = sh.llen[q][l];
+    if (g.stamps && tid == 0) g.stamps[t * 5 + 2] = wall_clock64();
+    // ---- per return column: compaction, pairwise tree, mean -------------------------------------
+    for (int q = 0; q < 3; ++q) {
         const double* x = fr0 + q * plane;
-        // first row of the leaf: the word holding compacted position off, then its bit
-        int lo = 0, hi = nw;                           // last word with pre <= off
-        while (hi - lo > 1) {
-            const int m = (lo + hi) >> 1;
-            if (sh.pre[q][m] <= off) lo = m; else hi = m;
+        const int n = sh.pre[q][nw];
+        for (int w = wave; w < nw; w += 4) {
+            const u64 m = sh.mw[q][w];
+            if ((m >> lane) & 1ull)
+                scr[sh.pre[q][w] + __popcll(m & ((1ull << lane) - 1ull))] = x[(int64_t)w * 64 + lane];
         }
-        int w = lo;
-        u64 rest = sh.mw[q][w];
-        for (int s = off - sh.pre[q][w]; s > 0; --s) rest &= rest - 1;
-        auto next = [&]() -> int64_t {                 // asset of the next compacted row
-            while (rest == 0ull) rest = sh.mw[q][++w];
-            const int64_t a = (int64_t)w * 64 + __builtin_ctzll(rest);
-            rest &= rest - 1;
-            return a;
-        };
-        double res;
-        if (len < 8) {
-            res = 0.;
-            for (int i = 0; i < len; ++i) res += x[next()];
-        } else {
-            double r[8];
-            int64_t ix[8];
+        if (tid == 0) {
+            sh.noff[0] = 0;
+            sh.nlen[0] = n;
+            sh.lvl[0] = 0;
+            sh.lvl[1] = 1;
+        }
+        __syncthreads();
+        int nlev = 0;
+        for (;;) {                                      // build the levels; sum their leaves
+            const int lb = sh.lvl[nlev], le = sh.lvl[nlev + 1];
+            if (le == lb) break;                        // (uniform)
+            int base = le;
+            for (int c0 = lb; c0 < le; c0 += kPT) {
+                const int i = c0 + tid;
+                const int m = i < le ? sh.nlen[i] : 0;
+                const int split = m > 128;
+                int ex;
+                const int tot = block_scan<kPT>(split, sh.scan, &ex);
+                if (i < le) {
+                    if (split) {
+                        int m2 = m / 2;
+                        m2 -= m2 % 8;
+                        const int ci = base + 2 * ex;
+                        sh.nchild[i] = ci;
+                        sh.noff[ci] = sh.noff[i];
+                        sh.nlen[ci] = m2;
+                        sh.noff[ci + 1] = sh.noff[i] + m2;
+                        sh.nlen[ci + 1] = m - m2;
+                    } else {
+                        sh.nchild[i] = -1;
+                        const double* a = scr + sh.noff[i];
+                        double res;
+                        if (m < 8) {
+                            res = 0.;
+                            for (int j = 0; j < m; ++j) res += a[j];
+                        } else {
+                            double r[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ix[j] = next();
+                            for (int j = 0; j < 8; ++j) r[j] = a[j];
+                            int j;
+                            for (j = 8; j < m - (m % 8); j += 8) {
+                                double v8[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) r[j] = x[ix[j]];
-            int i;
-            for (i = 8; i < len - (len % 8); i += 8) {
+                                for (int u = 0; u < 8; ++u) v8[u] = a[j + u];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) ix[j] = next();
-                double v8[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v8[j] = x[ix[j]];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) r[j] += v8[j];
+                                for (int u = 0; u < 8; ++u) r[u] += v8[u];
+                            }
+                            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                            for (; j < m; ++j) res += a[j];
+                        }
+                        sh.nval[i] = res;
+                    }
+                }
+                base += 2 * tot;
             }
-            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-            for (; i < len; ++i) res += x[next()];
+            if (tid == 0) sh.lvl[nlev + 2] = base;
+            __syncthreads();
+            ++nlev;
         }
-        sh.lval[q][l] = res;
+        for (int l = nlev - 2; l >= 0; --l) {           // internal nodes, bottom-up
+            for (int i = sh.lvl[l] + tid; i < sh.lvl[l + 1]; i += kPT) {
+                const int ci = sh.nchild[i];
+                if (ci >= 0) sh.nval[i] = sh.nval[ci] + sh.nval[ci + 1];
+            }
+            __syncthreads();
+        }
+        if (tid == 0) sh.mu[q] = n > 0 ? (0.0 + sh.nval[0]) / (double)n : qnan();
+        __syncthreads();
     }
-    __syncthreads();
-    if (tid < 3) {
-        const int n = sh.pre[tid][nw];
-        sh.mu[tid] = n > 0 ? (0.0 + pw_tree(n, sh.lval[tid])) / (double)n : qnan();
-    }
-    __syncthreads();
+    if (g.stamps && tid == 0) g.stamps[t * 5 + 3] = wall_clock64();
     // ---- surviving rows (all three returns), compacted, returns demeaned ----------------------
     const double mu0 = sh.mu[0], mu1 = sh.mu[1], mu2 = sh.mu[2];
     for (int w = wave; w < nw; w += 4) {
@@ -388,6 +355,7 @@ __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
         g.rows_idx[o] = (int32_t)a;
     }
     if (tid == 0) g.nrows[t] = sh.pre[2][nw];
+    if (g.stamps && tid == 0) { g.stamps[t * 5 + 4] = wall_clock64(); g.clk[t * 2 + 1] = clock64(); }
 }
 
 // ---- A3/A4: exact ranks -------------------------------------------------------------------
@@ -799,11 +767,40 @@ extern "C" int afm_xs_prepare_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t ld
                                   const double* sig, const double* fr, double* scratch,
                                   double* rows, int32_t* rows_idx, int32_t* nrows) {
     AFM_CTX(ctx);
-    AFM_CHECK_ARG(T > 0 && A > 0 && lda >= A && lda % 64 == 0 && A <= 65536, "bad shape");
+    AFM_CHECK_ARG(T > 0 && A > 0 && lda >= A && lda % 64 == 0 && A <= 64 * kMaxWords,
+                  "bad shape (A <= 32768)");
     AFM_CHECK_ARG(sig && fr && scratch && rows && rows_idx && nrows, "null buffer");
-    PrepArgs g{T, lda, A, sig, fr, scratch, rows, rows_idx, nrows};
+    PrepArgs g{T, lda, A, sig, fr, scratch, rows, rows_idx, nrows, nullptr, nullptr};
+    const bool probe = getenv("AFM_AN_PROBE") != nullptr;
+    if (probe) AFM_HIP(hipMalloc((void**)&g.stamps, sizeof(int64_t) * T * 5));
+    if (probe) AFM_HIP(hipMalloc((void**)&g.clk, sizeof(int64_t) * T * 2));
     hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)T), dim3(kPT), 0, ctx->stream, g);
     AFM_HIP(hipGetLastError());
+    if (probe) {                       // experiment: mean phase durations per date (100 MHz clock)
+        std::vector<int64_t> h((size_t)T * 5);
+        AFM_HIP(hipMemcpy(h.data(), g.stamps, sizeof(int64_t) * T * 5, hipMemcpyDeviceToHost));
+        double acc[4] = {0, 0, 0, 0};
+        int64_t t0 = h[0], t1 = h[4];
+        for (int64_t t = 0; t < T; ++t) {
+            for (int j = 0; j < 4; ++j) acc[j] += (double)(h[t * 5 + j + 1] - h[t * 5 + j]);
+            t0 = std::min(t0, h[t * 5]);
+            t1 = std::max(t1, h[t * 5 + 4]);
+        }
+        fprintf(stderr, "xs_prepare phases (us/date): masks %.1f prefix %.1f means %.1f rows %.1f; "
+                "span %.1f us\n", acc[0] / T / 100, acc[1] / T / 100, acc[2] / T / 100,
+                acc[3] / T / 100, (t1 - t0) / 100.0);
+        std::vector<int64_t> c((size_t)T * 2);
+        AFM_HIP(hipMemcpy(c.data(), g.clk, sizeof(int64_t) * T * 2, hipMemcpyDeviceToHost));
+        double cyc = 0, wall = 0;
+        for (int64_t t = 0; t < T; ++t) {
+            cyc += (double)(c[t * 2 + 1] - c[t * 2]);
+            wall += (double)(h[t * 5 + 4] - h[t * 5]);
+        }
+        fprintf(stderr, "shader clock %.0f MHz (clock64 ticks per 100 MHz wall tick x 100)\n",
+                wall > 0 ? cyc / wall * 100.0 : 0.0);
+        AFM_HIP(hipFree(g.stamps));
+        AFM_HIP(hipFree(g.clk));
+    }
     return AFM_OK;
 }
 

@@ -1,0 +1,65 @@
+"""Time the analyzer kernels one at a time on the bench workload (pipeline state after one
+step): the isolated latency of each stage of Pipeline._analyzer.
+    python tools/an_probe.py"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "alpha-multi-factor-models_amd")]
+
+
+def main():
+    import numpy as np
+    import torch
+    import afm
+    from afm import _lib
+    from afm.pipeline import Pipeline
+    from afm.synthetic import make_panel
+    p = make_panel(10000, 5040, seed=2023, tradable_p=0.9)
+    pipe = Pipeline(afm.PanelGrid.from_panel(p))
+    pipe.step()
+    torch.cuda.synchronize()
+    L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+    full, sp, an = pipe.full, pipe.sp, pipe.an
+    T, lda, a0, Ta = pipe.T, full.lda, pipe.an_a0, pipe.Ta
+    h = pipe.ctx.bind_stream()
+    cb = a0 // 64
+    calls = {
+        "fwd_returns": lambda: L.afm_fwd_returns_f64(h, Ta, lda, P(full.close[a0:]),
+                                                     P(pipe.price_bits[cb:]), P(an["fr"])),
+        "xs_prepare": lambda: L.afm_xs_prepare_f64(h, Ta, full.A, lda, P(pipe.pred[a0:]),
+                                                   P(an["fr"]), P(an["scratch"]), P(an["rows"]),
+                                                   P(an["rows_idx"]), P(an["nrows"])),
+        "xs_rank": lambda: L.afm_xs_rank_f64(h, Ta, lda, P(an["rows"]), P(an["nrows"]),
+                                             P(an["skey"]), P(an["sidx"]), P(an["ra"]),
+                                             P(an["rd"])),
+        "xs_stats": lambda: L.afm_xs_stats_f64(h, Ta, lda, P(pipe.an_dates), pipe.an_nd,
+                                               P(an["rows"]), P(an["nrows"]), P(an["ra"]),
+                                               P(an["rd"]), 10, P(an["ic"]), P(an["layer_mean"]),
+                                               P(an["layer_cnt"]), P(an["port"])),
+        "xs_series": lambda: L.afm_xs_series_f64(h, pipe.an_nd, P(an["layer_mean"]), P(an["port"]),
+                                                 P(an["ic"]), P(pipe.an_year), pipe.an_nyears,
+                                                 pipe.an_year0, P(an["cum_layer"]), P(an["ls"]),
+                                                 P(an["cum_port"]), P(an["ir"]),
+                                                 P(an["ir_scratch"])),
+        "pnl_scan": lambda: L.afm_pnl_scan_f64(h, pipe.nd, P(pipe.reb["k"]), P(pipe.reb["books"]),
+                                               P(pipe.reb["sums"]), P(pipe.reb["upos"]),
+                                               P(pipe.reb["usize"]), pipe.cfg.v0, pipe.cfg.rate,
+                                               P(pipe.pnl["value"]), P(pipe.pnl["turnover"]),
+                                               P(pipe.pnl["long_ret"]), P(pipe.pnl["short_ret"])),
+    }
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    print(f"analyzer grid {Ta} dates x {lda}; nrows mean {an['nrows'].float().mean().item():.0f}")
+    for name, fn in calls.items():
+        ts = []
+        for _ in range(5):
+            ev[0].record()
+            chk(fn(), name)
+            ev[1].record()
+            torch.cuda.synchronize()
+            ts.append(ev[0].elapsed_time(ev[1]))
+        print(f"{name}: {np.median(ts) * 1e3:.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
