@@ -522,34 +522,69 @@ __global__ __launch_bounds__(128) void xs_stats_kernel(StatArgs g) {
                 pv_has[rd - 1] = 1;
             }
         }
-        __syncthreads();
+        // one flag for the chunk: every staged value finite (the analyzer's rows always are)
+        int fin = 1;
+        for (int e = tid; e < len; e += 128)
+            fin &= __builtin_isfinite(sv[0][e]) && __builtin_isfinite(sv[1][e]) &&
+                   __builtin_isfinite(sv[2][e]) && __builtin_isfinite(sv[3][e]);
+        const bool all_fin = __syncthreads_and(fin);
         if (wave == 0 && lane < 3) {
             const double* R = sv[1 + k0];
-            for (int e = 0; e < len; ++e) {
-                const double vy = sv[0][e], vx = R[e];
-                if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
-                    nobs += 1;
+            if (all_fin && nobs == (double)c0) {
+                // no row skipped so far: nobs == row number, 1 / nobs from the table, no branch
+#pragma unroll 4
+                for (int e = 0; e < len; ++e) {
+                    const double vy = sv[0][e], vx = R[e], inv = sinv[e];
                     const double dx = vx - mx, dy = vy - my;
-                    // the same value as 1. / nobs, off the dependency chain while no row is skipped
-                    const double inv = nobs == (double)(c0 + e + 1) ? sinv[e] : 1. / nobs;
                     mx += inv * dx;
                     my += inv * dy;
                     sxx += (vx - mx) * dx;
                     syy += (vy - my) * dy;
                     sxy += (vx - mx) * dy;
                 }
+                nobs += (double)len;
+            } else {
+                for (int e = 0; e < len; ++e) {
+                    const double vy = sv[0][e], vx = R[e];
+                    if (__builtin_isfinite(vx) && __builtin_isfinite(vy)) {
+                        nobs += 1;
+                        const double dx = vx - mx, dy = vy - my;
+                        const double inv = nobs == (double)(c0 + e + 1) ? sinv[e] : 1. / nobs;
+                        mx += inv * dx;
+                        my += inv * dy;
+                        sxx += (vx - mx) * dx;
+                        syy += (vy - my) * dy;
+                        sxy += (vx - mx) * dy;
+                    }
+                }
             }
-        } else if (wave == 1 && lane < 3 * kLayers) {
-            const double* R = sv[1 + k1];
-            for (int e = 0; e < len; ++e) {
-                const double vx = R[e];
-                if (slay[e] == l1 && vx == vx) {
-                    lcnt += 1;
-                    const double y = vx - lcomp;
-                    const double tt = lsum + y;
-                    lcomp = tt - lsum - y;
-                    if (lcomp != lcomp) lcomp = 0;
-                    lsum = tt;
+        } else if (wave == 1) {
+            // each lane (type k1, layer l1) walks only its layer's rows: per 64-row group, one
+            // ballot per layer, then the set bits in row order
+            const double* R = sv[1 + (k1 < 3 ? k1 : 0)];
+            for (int g0 = 0; g0 < len; g0 += 64) {
+                const int e = g0 + lane;
+                const int myl = e < len ? slay[e] : -1;
+                u64 mine = 0ull;
+#pragma unroll
+                for (int l = 0; l < kLayers; ++l) {
+                    const u64 m = __ballot(myl == l);
+                    if (l == l1) mine = m;
+                }
+                if (lane < 3 * kLayers) {
+                    while (mine) {
+                        const int b = __builtin_ctzll(mine);
+                        mine &= mine - 1;
+                        const double vx = R[g0 + b];
+                        if (vx == vx) {
+                            lcnt += 1;
+                            const double y = vx - lcomp;
+                            const double tt = lsum + y;
+                            lcomp = tt - lsum - y;
+                            if (lcomp != lcomp) lcomp = 0;
+                            lsum = tt;
+                        }
+                    }
                 }
             }
         }
