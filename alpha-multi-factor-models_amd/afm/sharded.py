@@ -96,3 +96,38 @@ def ShardedPipeline(grid: PanelGrid, comm: Comm, cfg: PipelineConfig | None = No
     """``Pipeline.step()`` on one rank of ``comm.world`` (afm.pipeline.Pipeline with a comm):
     bit-identical to the single-device step for N in {1, 2, 4, 8}."""
     return Pipeline(grid, cfg, comm)
+
+
+def gather_path_series(local: dict, npaths: int, comm: Comm) -> dict:
+    """The per-path series of every rank's path share (``even_range`` of ``npaths``) in ONE
+    all-gather (shares padded to the largest) -> the full [npaths][...] series on every rank."""
+    import torch
+    keys = ("value", "turnover", "long_ret", "short_ret")
+    nmax = -(-npaths // comm.world)
+    padded = []
+    for k in keys:
+        t = local[k]
+        pad = torch.zeros((nmax,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[:t.shape[0]] = t
+        padded.append(pad)
+    got = comm.all_gather_packed(padded)
+    out = {}
+    for k, g in zip(keys, got):
+        parts = []
+        for q in range(comm.world):
+            lo, hi = even_range(npaths, comm.world, q)
+            parts.append(g[q, :hi - lo])
+        out[k] = torch.cat(parts)
+    return out
+
+
+def bootstrap_pnl_sharded(reb: dict, pred, dates_idx, paths, comm: Comm, v0=None, rate=1e-4):
+    """Config E on N GPUs: the bootstrap paths split evenly over the ranks (each path's value /
+    turnover recursion is independent -- no exchange while they run), then one all-gather of the
+    PnL series.  ``reb`` / ``pred`` are the (replicated) rebalance outputs of the sharded step."""
+    import numpy as np
+    from .portfolio import V0, bootstrap_pnl
+    paths = np.asarray(paths, dtype=np.int32)
+    lo, hi = even_range(len(paths), comm.world, comm.rank)
+    local = bootstrap_pnl(reb, pred, dates_idx, paths[lo:hi], V0 if v0 is None else v0, rate)
+    return gather_path_series(local, len(paths), comm)

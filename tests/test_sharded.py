@@ -11,6 +11,7 @@ import socket
 import sys
 
 import numpy as np
+from pathlib import Path
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -123,6 +124,30 @@ def test_subtree_exchange_is_bit_identical(tmp_path, world):
     assert all((tmp_path / f"tree{q}").exists() for q in range(world))
 
 
+def _paths_worker(rank, world, port, outdir):
+    import torch
+    _init(rank, world, port)
+    from afm.sharded import Comm, even_range, gather_path_series
+    npaths, steps = 11, 5
+    lo, hi = even_range(npaths, world, rank)
+    loc = {k: torch.arange(lo, hi, dtype=torch.float64)[:, None] * 10 + torch.arange(steps + (k == "value"))
+           for k in ("value", "turnover", "long_ret", "short_ret")}
+    out = gather_path_series(loc, npaths, Comm())
+    want = torch.arange(npaths, dtype=torch.float64)[:, None] * 10
+    assert torch.equal(out["value"], want + torch.arange(steps + 1))
+    assert torch.equal(out["turnover"], want + torch.arange(steps))
+    (Path(outdir) / f"paths{rank}").write_text("ok")
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_path_shards_gather(tmp_path, world):
+    """Config E sharding: uneven path shares, one packed all-gather, rows back in path order."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    mp.spawn(_paths_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / f"paths{q}").exists() for q in range(world))
+
+
 def test_shard_geometry():
     """Ranks own whole blocks of the fixed 8-block split (64-aligned, covering every asset)."""
     from afm.pipeline import N_BLOCKS, block_assets
@@ -153,8 +178,14 @@ def _sharded_worker(rank, world, port, outdir, A, T):
     sp.step()
     sp.step()
     torch.cuda.synchronize()
+    from afm.portfolio import bootstrap_paths
+    from afm.sharded import bootstrap_pnl_sharded
+    paths = bootstrap_paths(sp.nd, 37, seed=5)               # 37 paths: uneven rank shares
+    boot = bootstrap_pnl_sharded(sp.reb, sp.pred, sp.rdates, paths, Comm(), rate=sp.cfg.rate)
+    torch.cuda.synchronize()
     if rank == 0:
         np.savez(os.path.join(outdir, "sharded.npz"), pool=sp.pool_g.cpu().numpy(),
+                 boot=boot["value"].cpu().numpy(), boot_to=boot["turnover"].cpu().numpy(),
                  beta=sp.lasso_beta.cpu().numpy(), pred=sp.pred.cpu().numpy(),
                  fm=sp.fm_beta.cpu().numpy(), fm_mean=sp.fm_mean.cpu().numpy(),
                  k=sp.reb["k"].cpu().numpy(), books=sp.reb["books"].cpu().numpy(),
@@ -167,7 +198,8 @@ def _sharded_worker(rank, world, port, outdir, A, T):
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_ranks_bit_identical_to_single(tmp_path, world):
     """N ranks (gloo, sharing cuda:0) run the whole step: the pooled Gram, Lasso, predictions,
-    FM betas, books, weights, PnL and IC are BIT-identical to the one-device step."""
+    FM betas, books, weights, PnL and IC are BIT-identical to the one-device step; so are the
+    config-E bootstrap paths sharded over the ranks."""
     import torch
     import torch.multiprocessing as mp
     import afm
@@ -197,3 +229,9 @@ def test_sharded_ranks_bit_identical_to_single(tmp_path, world):
     ic = pipe.an["ic"].cpu().numpy()
     assert np.array_equal(np.isnan(s["ic"]), np.isnan(ic))
     assert np.array_equal(s["ic"][~np.isnan(ic)], ic[~np.isnan(ic)])
+    # config E: paths sharded over the ranks + one all-gather == all paths on one device
+    from afm.portfolio import bootstrap_paths, bootstrap_pnl
+    one = bootstrap_pnl(pipe.reb, pipe.pred, pipe.rdates, bootstrap_paths(pipe.nd, 37, seed=5),
+                        rate=pipe.cfg.rate)
+    assert np.array_equal(s["boot"], one["value"].cpu().numpy())
+    assert np.array_equal(s["boot_to"], one["turnover"].cpu().numpy())
