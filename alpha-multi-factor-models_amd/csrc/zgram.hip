@@ -42,7 +42,7 @@ constexpr int kZRS = 66;                     // LDS row stride (doubles): confli
 constexpr int kZMaxSlots = 3;                // ring depth (2 when p + 4 staged rows do not fit 3x)
 constexpr int kZLds = 160 * 1024 - 256;      // dynamic LDS budget of the ring
 constexpr int kZProd = 8;                    // producer waves
-constexpr int kZThreads = 12 * 64;           // 8 producers + up to 4 consumers
+constexpr int kZThreads = 13 * 64;           // 8 producers + up to 4 consumers + border wave
 
 // Shapes: NT 16-wide tiles (NT = 7: p + 2 <= 108, the 97-feature design; NT = 2: p + 2 <= 32,
 // the FM30 design).  Consumer wave c owns tile pairs [c * PPW, (c + 1) * PPW) of the J-major
@@ -52,9 +52,21 @@ struct ZCfg {
     static constexpr int NP = NT * (NT + 1) / 2;
     static constexpr int PE = NP * 256;                        // doubles of one partial
     static constexpr int NCW = NT == 7 ? 4 : 3;                // consumer waves
-    static constexpr int PPW = (NP + NCW - 1) / NCW;           // pairs per consumer wave
+    // NT = 7: the columns of the last tile (96 .. p+1, at most 12) go to the border wave's VALU
+    // sums; the MFMA consumers take the 21 pairs of tiles 0..5 -- 3 on wave 0 (which shares SIMD 0
+    // with the border wave), 6 on each of waves 1..3.  NT = 2: all 3 pairs, one per wave.
+    static constexpr bool BORDER = NT == 7;
+    static constexpr int NMP = BORDER ? (NT - 1) * NT / 2 : NP;   // MFMA pairs
+    static constexpr int NWAIT = NCW + (BORDER ? 1 : 0);          // waves that free a slot
     static constexpr int KMAX = NT == 7 ? 108 : 16 * NT;       // staged columns p + 2 <= KMAX
     static constexpr int MC = (KMAX + kZProd - 1) / kZProd;    // columns per producer wave
+    static constexpr int q0(int cw) {
+        return BORDER ? (cw == 0 ? 0 : 3 + 6 * (cw - 1)) : cw * ((NMP + NCW - 1) / NCW);
+    }
+    static constexpr int nq(int cw) {
+        return BORDER ? (cw == 0 ? 3 : 6)
+                      : (q0(cw) + (NMP + NCW - 1) / NCW <= NMP ? (NMP + NCW - 1) / NCW : NMP - q0(cw));
+    }
 };
 
 template <int NT>
@@ -250,7 +262,7 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, con
             zload(B.zoff);
             zitem = B.item;
         }
-        wait_count(&sm.freed[slot], ZCfg<NT>::NCW * gen);
+        wait_count(&sm.freed[slot], ZCfg<NT>::NWAIT * gen);
         lds_double* tb = sm.tile + slot * sm.slot_elems + lane;
 #pragma unroll
         for (int j = 0; j < MC; ++j) {
@@ -287,8 +299,8 @@ template <int NT, int CW>
 __device__ void zgram_consume(const ZGramArgs& g, ZSmem& sm, const int lane) {
     using Cf = ZCfg<NT>;
     constexpr ZPairs<NT> tab{};
-    constexpr int Q0 = CW * Cf::PPW;
-    constexpr int NQ = (Q0 + Cf::PPW <= Cf::NP ? Cf::PPW : Cf::NP - Q0);
+    constexpr int Q0 = Cf::q0(CW);
+    constexpr int NQ = Cf::nq(CW);
     constexpr int THI = tab.J[Q0 + NQ - 1] + 1;                // tiles [0, THI) are touched
     const int fi = lane & 15, kk = lane >> 4;
     const int p = g.p;
@@ -357,6 +369,92 @@ __device__ void zgram_consume(const ZGramArgs& g, ZSmem& sm, const int lane) {
     }
 }
 
+// The border wave (NT = 7): the Gram columns b = 96 .. p+1 (at most 12; p = 97: z_96, z_97, y)
+// against every column c, as VALU sums over the staged rows -- lanes own columns c = lane,
+// lane + 64, the border values are broadcast reads.  It shares SIMD 0 with the lightest MFMA
+// consumer: f64 VALU and MFMA issue from separate pipes.  An item's last row-block flushes the
+// sums into the partial's (c / 16, 6) tile pairs in the MFMA C/D layout, so the trees and the
+// final symmetric write are unchanged.
+__device__ __forceinline__ double rdlane_d(double v, int l) {     // l uniform
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int NT, int NB>
+__device__ void zgram_border(const ZGramArgs& g, ZSmem& sm, const int lane) {
+    constexpr ZPairs<NT> tab{};
+    const int K = g.p + 2;
+    double acc[2][NB];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[cc][b] = 0.0;
+    int slot = 0, gen = 1;
+    Seq cur;
+    for (cur.init(g); cur.valid(); cur.advance(g)) {
+        wait_count(&sm.ready[slot], kZProd * gen);
+        // per row: the lane's two column values, and the NB border values as uniform-address
+        // (broadcast) reads -- all independent of the sums, so an unrolled group is in flight
+        const lds_double* tb = sm.tile + slot * sm.slot_elems;
+        const lds_double* c0 = tb + lane * kZRS;
+        const lds_double* c1 = tb + (lane + 64 < K ? lane + 64 : g.p + 2) * kZRS;  // zero row
+        const lds_double* bb = tb + 96 * kZRS;
+#pragma unroll 8
+        for (int r = 0; r < 64; ++r) {
+            const double x0 = c0[r], x1 = c1[r];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const double zb = bb[b * kZRS + r];
+                acc[0][b] = __builtin_fma(x0, zb, acc[0][b]);
+                acc[1][b] = __builtin_fma(x1, zb, acc[1][b]);
+            }
+        }
+        signal_count(&sm.freed[slot], lane);
+        if (++slot == sm.nslots) { slot = 0; ++gen; }
+        if (cur.last()) {
+            double* out = g.part + (int64_t)cur.item * ZCfg<NT>::PE;
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const int c = lane + 64 * cc;
+                if (c < K) {
+                    const int ti = c >> 4, w = c & 15;
+                    int q = 0;                                     // pair (ti, 6)
+#pragma unroll
+                    for (int qq = 0; qq < ZCfg<NT>::NP; ++qq)
+                        if (tab.I[qq] == ti && tab.J[qq] == NT - 1) q = qq;
+                    const int r4 = w >> 2, lrow = (w & 3) * 16;
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) out[q * 256 + r4 * 64 + lrow + b] = acc[cc][b];
+                }
+#pragma unroll
+                for (int b = 0; b < NB; ++b) acc[cc][b] = 0.0;
+            }
+        }
+    }
+}
+
+// the border wave for any border width 1..12 (the pooled design has 3: z_96, z_97, y)
+template <int NT>
+__device__ void zgram_border_any(const ZGramArgs& g, ZSmem& sm, const int lane) {
+    switch (g.p + 2 - 96) {
+        case 1: zgram_border<NT, 1>(g, sm, lane); break;
+        case 2: zgram_border<NT, 2>(g, sm, lane); break;
+        case 3: zgram_border<NT, 3>(g, sm, lane); break;
+        case 4: zgram_border<NT, 4>(g, sm, lane); break;
+        case 5: zgram_border<NT, 5>(g, sm, lane); break;
+        case 6: zgram_border<NT, 6>(g, sm, lane); break;
+        case 7: zgram_border<NT, 7>(g, sm, lane); break;
+        case 8: zgram_border<NT, 8>(g, sm, lane); break;
+        case 9: zgram_border<NT, 9>(g, sm, lane); break;
+        case 10: zgram_border<NT, 10>(g, sm, lane); break;
+        case 11: zgram_border<NT, 11>(g, sm, lane); break;
+        case 12: zgram_border<NT, 12>(g, sm, lane); break;
+        default: zgram_border<NT, 0>(g, sm, lane); break;   // no border columns: just free slots
+    }
+}
+
 template <int NT, int MODE, bool ZS>
 __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int nslots, int prio) {
     extern __shared__ __attribute__((aligned(16))) double ring[];
@@ -373,7 +471,7 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
     }
     if (tid < kZMaxSlots) { sm.ready[tid] = 0; sm.freed[tid] = 0; }
     __syncthreads();
-    if (wave >= 4) {
+    if (wave >= 4 && wave < 4 + kZProd) {
         if (prio & 1) __builtin_amdgcn_s_setprio(1);
         if (!AFM_ZG_TPL) {
             zgram_produce<NT, MODE, ZS, 0>(g, sm, lane, wave - 4);
@@ -389,6 +487,12 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
                 default: zgram_produce<NT, MODE, ZS, 7>(g, sm, lane, 7); break;
             }
         }
+        return;
+    }
+    if (wave == 12) {
+        // VALU-bound and on every slot's critical path: ahead of the producers' VALU on SIMD 0
+        __builtin_amdgcn_s_setprio(2);
+        if constexpr (ZCfg<NT>::BORDER) zgram_border_any<NT>(g, sm, lane);
         return;
     }
     if (prio & 2) __builtin_amdgcn_s_setprio(2);
