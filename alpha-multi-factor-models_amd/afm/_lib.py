@@ -53,6 +53,7 @@ SIGNATURES = {
     "afm_min_variance_weights_f64": (I32, [P, P, I64, I64, I32, DBL, DBL, P, P, P]),
     "afm_fwd_returns_f64": (I32, [P, I64, I64, P, P, P]),
     "afm_xs_prepare_f64": (I32, [P, I64, I64, I64, P, P, P, P, P, P]),
+    "afm_xs_prepare_range_f64": (I32, [P, I64, I64, I64, I64, I64, P, P, P, P, P, P]),
     "afm_xs_rank_f64": (I32, [P, I64, I64, P, P, P, P, P, P]),
     "afm_xs_stats_f64": (I32, [P, I64, I64, P, I64, P, P, P, P, I32, P, P, P, P]),
     "afm_xs_series_f64": (I32, [P, I64, P, P, P, P, I32, I32, P, P, P, P, P]),

@@ -302,6 +302,11 @@ class Pipeline:
             ad = np.arange(sp.s0 - self.an_a0, Ta, dtype=np.int32)   # test dates, sub-grid index
             self.an_dates = torch.from_numpy(ad).to(dev)
             self.an_nd = nad = len(ad)
+            # N > 1: each rank evaluates an even share of the test dates (every stage of the
+            # analyzer but the final series is per date); one packed all-gather of the per-date
+            # results, then every rank runs the series
+            self.an_rng = _even(nad, W, rk) if W > 1 else (0, nad)
+            self.an_nmax = max(b - a for a, b in (_even(nad, W, q) for q in range(W)))
             years = np.asarray(grid.dates).astype("datetime64[Y]").astype(np.int64) + 1970
             yr = years[self.an_a0 + ad].astype(np.int32)
             self.an_year0, self.an_nyears = int(yr.min()), int(yr.max() - yr.min() + 1)
@@ -508,11 +513,32 @@ class Pipeline:
             if W > 1:          # FM: per-date subtrees -> date owners (issued after the main chain)
                 self.main.wait_stream(self.side)
                 self._fm_exchange()
+                if c.analyzer:  # the analyzer's per-date results, then its series (last: RCCL
+                    with torch.cuda.stream(self.side2):     # runs a group's collectives in order)
+                        self._analyzer_series(mark)
         for s in (self.main, self.side, self.side2):
             caller.wait_stream(s)
         self.ctx.bind_stream()
 
     # ---- exchanges (N > 1) -------------------------------------------------------------------
+    def _gather_analyzer(self):
+        """The per-date analyzer results of every rank's date share -> the full arrays (one
+        packed all-gather, shares padded to the largest)."""
+        import torch
+        an, (j0, j1), n = self.an, self.an_rng, self.an_nmax
+        keys = ("ic", "layer_mean", "layer_cnt", "port")
+        pads = []
+        for k in keys:
+            t = an[k]
+            pad = torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            pad[:j1 - j0] = t[j0:j1]
+            pads.append(pad)
+        got = self.comm.all_gather_packed(pads)
+        for k, g in zip(keys, got):
+            for q in range(self.W):
+                a, b = _even(self.an_nd, self.W, q)
+                an[k][a:b] = g[q, :b - a]
+
     def _place(self, dst, gathered, rows=None):
         """Scatter per-rank shard columns ([W][rows][wide]) into a full-width plane."""
         for q, (lo, hi) in enumerate(self.ranges):
@@ -591,15 +617,30 @@ class Pipeline:
         cb = a0 // 64
         chk(L.afm_fwd_returns_f64(h, Ta, lda, P(full.close[a0:]), P(self.price_bits[cb:]),
                                   P(an["fr"])), "fwd_returns")
-        chk(L.afm_xs_prepare_f64(h, Ta, full.A, lda, P(self.pred[a0:]), P(an["fr"]),
-                                 P(an["scratch"]), P(an["rows"]), P(an["rows_idx"]),
-                                 P(an["nrows"])), "xs_prepare")
-        chk(L.afm_xs_rank_f64(h, Ta, lda, P(an["rows"]), P(an["nrows"]), P(an["skey"]),
-                              P(an["sidx"]), P(an["ra"]), P(an["rd"])), "xs_rank")
-        chk(L.afm_xs_stats_f64(h, Ta, lda, P(self.an_dates), self.an_nd, P(an["rows"]),
-                               P(an["nrows"]), P(an["ra"]), P(an["rd"]), 10, P(an["ic"]),
-                               P(an["layer_mean"]), P(an["layer_cnt"]), P(an["port"])),
-            "xs_stats")
+        j0, j1 = self.an_rng
+        d0 = sp.s0 - a0 + j0                        # sub-grid dates [d0, d1) of this rank
+        d1 = d0 + (j1 - j0)
+        if j1 > j0:
+            chk(L.afm_xs_prepare_range_f64(h, Ta, full.A, lda, d0, d1, P(self.pred[a0:]),
+                                           P(an["fr"]), P(an["scratch"]), P(an["rows"]),
+                                           P(an["rows_idx"]), P(an["nrows"])), "xs_prepare")
+            chk(L.afm_xs_rank_f64(h, d1 - d0, lda, P(an["rows"][0, d0:]), P(an["nrows"][d0:]),
+                                  P(an["skey"][d0:]), P(an["sidx"][d0:]), P(an["ra"][d0:]),
+                                  P(an["rd"][d0:])), "xs_rank")
+            chk(L.afm_xs_stats_f64(h, Ta, lda, P(self.an_dates[j0:]), j1 - j0, P(an["rows"]),
+                                   P(an["nrows"]), P(an["ra"]), P(an["rd"]), 10, P(an["ic"][j0:]),
+                                   P(an["layer_mean"][j0:]), P(an["layer_cnt"][j0:]),
+                                   P(an["port"][j0:])), "xs_stats")
+        if self.W > 1:
+            return          # the all-gather and the series follow the main chain's exchanges
+        self._analyzer_series(mark)
+
+    def _analyzer_series(self, mark):
+        L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+        an = self.an
+        if self.W > 1:
+            self._gather_analyzer()
+        h = self.ctx.bind_stream()
         chk(L.afm_xs_series_f64(h, self.an_nd, P(an["layer_mean"]), P(an["port"]), P(an["ic"]),
                                 P(self.an_year), self.an_nyears, self.an_year0,
                                 P(an["cum_layer"]), P(an["ls"]), P(an["cum_port"]), P(an["ir"]),

@@ -181,6 +181,7 @@ struct PrepArgs {
     double* rows;             // [4][T][lda]: factor, r1, r2, r5 of surviving rows, compacted
     int32_t* rows_idx;        // [T][lda] asset index of each compacted row
     int32_t* nrows;           // [T] surviving rows per date
+    int64_t t0;               // first date processed (workgroup b: date t0 + b)
     int64_t* stamps;          // experiment (AFM_AN_PROBE): 5 phase timestamps per date, or null
     int64_t* clk;             // experiment: shader-clock stamps at phases 0 and 4
 };
@@ -211,7 +212,7 @@ struct PrepShared {
 __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
     __shared__ PrepShared sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t t = blockIdx.x;
+    const int64_t t = g.t0 + blockIdx.x;
     const int64_t plane = g.T * g.lda;
     const double* sig = g.sig + t * g.lda;
     const double* fr0 = g.fr + t * g.lda;
@@ -798,45 +799,46 @@ extern "C" int afm_fwd_returns_f64(afm_ctx* ctx, int64_t T, int64_t lda, const d
     return AFM_OK;
 }
 
-extern "C" int afm_xs_prepare_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
-                                  const double* sig, const double* fr, double* scratch,
-                                  double* rows, int32_t* rows_idx, int32_t* nrows) {
+extern "C" int afm_xs_prepare_range_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
+                                        int64_t t0, int64_t t1, const double* sig,
+                                        const double* fr, double* scratch, double* rows,
+                                        int32_t* rows_idx, int32_t* nrows) {
     AFM_CTX(ctx);
     AFM_CHECK_ARG(T > 0 && A > 0 && lda >= A && lda % 64 == 0 && A <= 64 * kMaxWords,
                   "bad shape (A <= 32768)");
+    AFM_CHECK_ARG(0 <= t0 && t0 <= t1 && t1 <= T, "bad date range");
     AFM_CHECK_ARG(sig && fr && scratch && rows && rows_idx && nrows, "null buffer");
-    PrepArgs g{T, lda, A, sig, fr, scratch, rows, rows_idx, nrows, nullptr, nullptr};
+    if (t1 == t0) return AFM_OK;
+    PrepArgs g{T, lda, A, sig, fr, scratch, rows, rows_idx, nrows, t0, nullptr, nullptr};
     const bool probe = getenv("AFM_AN_PROBE") != nullptr;
     if (probe) AFM_HIP(hipMalloc((void**)&g.stamps, sizeof(int64_t) * T * 5));
     if (probe) AFM_HIP(hipMalloc((void**)&g.clk, sizeof(int64_t) * T * 2));
-    hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)T), dim3(kPT), 0, ctx->stream, g);
+    hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)(t1 - t0)), dim3(kPT), 0, ctx->stream, g);
     AFM_HIP(hipGetLastError());
     if (probe) {                       // experiment: mean phase durations per date (100 MHz clock)
         std::vector<int64_t> h((size_t)T * 5);
         AFM_HIP(hipMemcpy(h.data(), g.stamps, sizeof(int64_t) * T * 5, hipMemcpyDeviceToHost));
         double acc[4] = {0, 0, 0, 0};
-        int64_t t0 = h[0], t1 = h[4];
-        for (int64_t t = 0; t < T; ++t) {
+        int64_t s0 = h[t0 * 5], s1 = h[t0 * 5 + 4];
+        for (int64_t t = t0; t < t1; ++t) {
             for (int j = 0; j < 4; ++j) acc[j] += (double)(h[t * 5 + j + 1] - h[t * 5 + j]);
-            t0 = std::min(t0, h[t * 5]);
-            t1 = std::max(t1, h[t * 5 + 4]);
+            s0 = std::min(s0, h[t * 5]);
+            s1 = std::max(s1, h[t * 5 + 4]);
         }
+        const double f = 1.0 / (double)(t1 - t0) / 100.0;
         fprintf(stderr, "xs_prepare phases (us/date): masks %.1f prefix %.1f means %.1f rows %.1f; "
-                "span %.1f us\n", acc[0] / T / 100, acc[1] / T / 100, acc[2] / T / 100,
-                acc[3] / T / 100, (t1 - t0) / 100.0);
-        std::vector<int64_t> c((size_t)T * 2);
-        AFM_HIP(hipMemcpy(c.data(), g.clk, sizeof(int64_t) * T * 2, hipMemcpyDeviceToHost));
-        double cyc = 0, wall = 0;
-        for (int64_t t = 0; t < T; ++t) {
-            cyc += (double)(c[t * 2 + 1] - c[t * 2]);
-            wall += (double)(h[t * 5 + 4] - h[t * 5]);
-        }
-        fprintf(stderr, "shader clock %.0f MHz (clock64 ticks per 100 MHz wall tick x 100)\n",
-                wall > 0 ? cyc / wall * 100.0 : 0.0);
+                "span %.1f us\n", acc[0] * f, acc[1] * f, acc[2] * f, acc[3] * f, (s1 - s0) / 100.0);
         AFM_HIP(hipFree(g.stamps));
         AFM_HIP(hipFree(g.clk));
     }
     return AFM_OK;
+}
+
+extern "C" int afm_xs_prepare_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
+                                  const double* sig, const double* fr, double* scratch,
+                                  double* rows, int32_t* rows_idx, int32_t* nrows) {
+    return afm_xs_prepare_range_f64(ctx, T, A, lda, 0, T, sig, fr, scratch, rows, rows_idx,
+                                    nrows);
 }
 
 extern "C" int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* rows,

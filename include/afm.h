@@ -207,10 +207,15 @@ int afm_fwd_returns_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* clos
 /* Per date: the merge/dropna cascade and per-date demeans of KKT:313-318 (numpy pairwise mean).
  * sig [T][lda] (NaN = no signal row).  Surviving rows, compacted in ascending asset order:
  * rows [4][T][lda] = {factor, return_1, return_2, return_5 (demeaned)}, rows_idx [T][lda] asset
- * index, nrows [T].  scratch [T][lda].  A <= 65536. */
+ * index, nrows [T].  scratch [T][lda].  A <= 32768. */
 int afm_xs_prepare_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, const double* sig,
                        const double* fr, double* scratch, double* rows, int32_t* rows_idx,
                        int32_t* nrows);
+/* afm_xs_prepare_f64 on the dates [t0, t1) of the [T]-date buffers only (a rank's share of the
+ * dates on N GPUs; T fixes the plane strides of fr and rows). */
+int afm_xs_prepare_range_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,
+                             int64_t t1, const double* sig, const double* fr, double* scratch,
+                             double* rows, int32_t* rows_idx, int32_t* nrows);
 /* Exact per-date ranks of the compacted factor column (method='first': ties by row order),
  * ascending and descending.  skey/sidx [T][lda] scratch. */
 int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* rows,
