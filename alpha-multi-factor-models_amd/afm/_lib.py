@@ -28,6 +28,8 @@ SIGNATURES = {
     "afm_version": (I32, []),
     "afm_factor_name": (ctypes.c_char_p, [I32]),
     "afm_factors_f64": (I32, [P, I64, I64, I64, P, P, P, P, P, P, P, P]),
+    "afm_factors_state_bytes": (I64, [P, I64]),
+    "afm_factors_slab_f64": (I32, [P, I64, I64, I64, I64, I64, P, P, P, P, P, P, P, P, P]),
     "afm_xs_gram_f64": (I32, [P, P, I64, I64, I64, I64, P, I32, I32, P, I64, I64, P, P]),
     "afm_ols_solve_f64": (I32, [P, P, P, I32, I64, DBL, P, P, P]),
     "afm_pool_moments_f64": (I32, [P, P, P, I32, I64, P, P]),

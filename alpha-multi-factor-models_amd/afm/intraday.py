@@ -7,11 +7,14 @@ one -- the grid's date axis simply holds bars.  What changes is size.  At 3,000 
 MI355X's 288 GB of HBM, and every recurrence is sequential over the whole 196,560-bar series
 (pandas' Kahan / Welford states carry their rounding history).
 
-So the build streams over **asset groups**: assets are independent, so each group of 64-asset
-blocks is an exact sub-panel.  ``factor_panel_groups`` slices the resident input planes into a
-group grid, runs ``afm_factors_f64`` into one reused output buffer sized to the free HBM, and
-hands each finished group to a consumer callback.  Results are bit-identical to a single launch
-over the whole panel (tests/test_intraday_gpu.py).
+So the build streams: ``factor_panel_slabs`` (the default) runs ALL assets over one TIME SLAB
+of bars at a time (``afm_factors_slab_f64``), carrying every recurrence state and observation
+ring from slab to slab in a device buffer, into one reused output buffer sized to the free HBM
+-- all 47 blocks of config D work at once, where asset groups would leave most CUs idle on a
+sequential 196,560-step scan.  ``factor_panel_groups`` streams asset groups instead (assets are
+independent, so each group of 64-asset blocks is an exact sub-panel).  Both hand each finished
+piece to a consumer callback and are bit-identical to a single launch over the whole panel
+(tests/test_intraday_gpu.py).
 
 ``make_panel_device`` is the §8(d) generator restated in torch on the device (same
 distributions, torch's RNG stream), because a 5.9e8-cell panel is slow to draw with numpy on
@@ -139,5 +142,59 @@ def factor_panel_groups(grid: PanelGrid, consumer, blocks_per_group: int | None 
         factor_panel(sub, out=o, nanfree=nf)
         consumer(a0, a1, o, nf)
         del sub
+        n += 1
+    return n
+
+
+def slab_bars(grid: PanelGrid, budget_bytes: int | None = None) -> int:
+    """Bars per time slab: the most (a multiple of 64) whose output planes and mask words fit in
+    ``budget_bytes`` (default: 85% of the free HBM), balanced so the slabs have near-equal
+    lengths."""
+    import torch
+    T, lda = grid.T, grid.lda
+    if budget_bytes is None:
+        free, _ = torch.cuda.mem_get_info(grid.device)
+        budget_bytes = int(free * 0.85)
+    per_bar = N_FACTORS * 8 * lda + 2 * 8 * lda // 64 + 16
+    cap = max(64, (budget_bytes // per_bar) // 64 * 64)
+    n = (T + cap - 1) // cap
+    return min(T, ((T + n - 1) // n + 63) // 64 * 64)
+
+
+def factor_panel_slabs(grid: PanelGrid, consumer, bars_per_slab: int | None = None):
+    """Build the 98-column factor panel of ``grid`` one time slab at a time, all assets at once.
+
+    ``consumer(t0, t1, out, nanfree)`` receives each slab: bars ``[t0, t1)``, ``out`` float64
+    ``[98][t1 - t0][lda]`` (absent cells stale -- consult ``nanfree``), ``nanfree`` int64
+    ``[ceil((t1 - t0)/64)][lda]``.  The buffers are reused by the next slab, so the consumer
+    must finish with them (on the current stream) before returning.  Returns the number of
+    slabs."""
+    import torch
+    from . import _lib
+    T, lda = grid.T, grid.lda
+    step = int(bars_per_slab) if bars_per_slab is not None else slab_bars(grid)
+    if step <= 0 or step % 64:
+        raise ValueError("bars_per_slab must be a positive multiple of 64")
+    ctx = _lib.Context.get(grid.device.index)
+    L, P = _lib.lib(), _lib.ptr
+    h = ctx.bind_stream()
+    nbytes = int(L.afm_factors_state_bytes(h, grid.A))
+    if nbytes < 0:
+        raise RuntimeError("afm_factors_state_bytes failed")
+    state = torch.empty(max(nbytes // 8, 1), dtype=torch.float64, device=grid.device)
+    out = torch.empty((N_FACTORS, min(step, T), lda), dtype=torch.float64, device=grid.device)
+    nanfree = torch.empty(((min(step, T) + 63) // 64, lda), dtype=torch.int64, device=grid.device)
+    n = 0
+    for t0 in range(0, T, step):
+        t1 = min(T, t0 + step)
+        m = t1 - t0
+        o = out if m == out.shape[1] else out.view(-1)[: N_FACTORS * m * lda].view(N_FACTORS, m, lda)
+        nw = (m + 63) // 64
+        nf = nanfree if nw == nanfree.shape[0] else nanfree[:nw]
+        _lib.check(L.afm_factors_slab_f64(ctx.bind_stream(), T, grid.A, lda, t0, t1,
+                                          P(grid.close), P(grid.volume), P(grid.ret1d),
+                                          P(grid.excess), P(grid.vbits), P(o), P(nf), None,
+                                          P(state)), "afm_factors_slab_f64")
+        consumer(t0, t1, o, nf)
         n += 1
     return n

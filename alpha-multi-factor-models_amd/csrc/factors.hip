@@ -132,6 +132,13 @@ struct Args {
     int fast;                  // 0: general step only (A/B tests)
     int nblk;                  // 64-asset blocks (paired launch: items = nblk * types)
     int pslot;                 // profiling build: block * types + type of the running item
+    // time slab [c0 * kChunk, t1) (c0 * kChunk a multiple of 64): out and the mask partials hold
+    // only the slab's dates (out is offset by the host so that date t's row is out + t * lda);
+    // state (or null) carries every wave's recurrence state and the loaders' rings across slabs
+    int c0, c1;                // chunk range of the slab
+    int64_t t1;                // slab end (exclusive)
+    GLB double* state;         // [nblk][types][jobs + 1][kStateWords][64]
+    int load_state;            // the slab continues a series: restore the state first
 };
 
 // Ring cell of lookback L (observation p - L) as a byte offset from row 0, given pmoff = the
@@ -792,26 +799,35 @@ using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>>;
 // The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
 // job waves (one per chunk + two at each 64-day word end).  It also publishes, per lane and
 // chunk, whether every present day of the chunk is clean (kClean).
-__device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane, int64_t block) {
+__device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane, int64_t block,
+                                          GLB double* st) {
     LDS Smem& sm = *smp;
     const int64_t asset = block * kLanes + lane;
-    const int nch = (int)((a.T + kChunk - 1) / kChunk);
+    const int c0 = a.c0, nch = a.c1;
     double pc[kChunk], pv[kChunk];
-    u64 vb = a.vbits[asset];
+    u64 vb = a.vbits[(int64_t)((c0 * kChunk) >> 6) * a.lda + asset];
     int pmod = 0;                                   // observations before the staged chunk, mod kRing
     int run = 0;                                    // consecutive in-range observations
+    if (st && a.load_state) {                       // the ring and counters of the previous slab
+        for (int q = 0; q < kRing; ++q) {
+            sm.c[q][lane] = st[(2 * q) * kLanes + lane];
+            sm.v[q][lane] = st[(2 * q + 1) * kLanes + lane];
+        }
+        pmod = (int)st[(2 * kRing) * kLanes + lane];
+        run = (int)st[(2 * kRing + 1) * kLanes + lane];
+    }
     auto load = [&](int ch) {
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
             const int64_t t = (int64_t)ch * kChunk + j;
-            const bool in = t < a.T;
+            const bool in = t < a.t1;
             pc[j] = in ? a.close[t * a.lda + asset] : 0.0;
             pv[j] = in ? a.volume[t * a.lda + asset] : 0.0;
         }
     };
     auto stage = [&](int ch) {                      // registers (chunk ch) -> ring + cbyte
         const int sh = (ch * kChunk) & 63;
-        if (sh == 0 && ch > 0) vb = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
+        if (sh == 0 && ch > c0) vb = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
         const u64 cb = (vb >> sh) & 0xffull;
         int q = pmod;
         bool ok = true;
@@ -830,11 +846,11 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         sm.cbyte[ch & 1][lane] = (int)cb;
         sm.okbyte[ch & 1][lane] = (a.fast && ok) ? 1 : 0;
     };
-    load(0);
-    stage(0);
-    if (nch > 1) load(1);
-    lds_barrier();                                  // chunk 0 staged
-    for (int ch = 0; ch < nch; ++ch) {
+    load(c0);
+    stage(c0);
+    if (c0 + 1 < nch) load(c0 + 1);
+    lds_barrier();                                  // chunk c0 staged
+    for (int ch = c0; ch < nch; ++ch) {
         if (ch + 1 < nch) {
             stage(ch + 1);
             if (ch + 2 < nch) load(ch + 2);
@@ -843,26 +859,55 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         if (sh + kChunk == 64 || ch + 1 == nch) { lds_barrier(); lds_barrier(); }
         lds_barrier();
     }
+    if (st) {                                       // for the next slab (after the last barrier:
+        for (int q = 0; q < kRing; ++q) {           // no job wave reads the ring any more)
+            st[(2 * q) * kLanes + lane] = sm.c[q][lane];
+            st[(2 * q + 1) * kLanes + lane] = sm.v[q][lane];
+        }
+        st[(2 * kRing) * kLanes + lane] = (double)pmod;
+        st[(2 * kRing + 1) * kLanes + lane] = (double)run;
+    }
 }
 
 // A wave with no item (odd item count in the paired launch): the loader's barrier sequence.
 __device__ __forceinline__ void idle_wave(const Args& a) {
-    const int nch = (int)((a.T + kChunk - 1) / kChunk);
+    const int nch = a.c1;
     lds_barrier();
-    for (int ch = 0; ch < nch; ++ch) {
+    for (int ch = a.c0; ch < nch; ++ch) {
         const int sh = (ch * kChunk) & 63;
         if (sh + kChunk == 64 || ch + 1 == nch) { lds_barrier(); lds_barrier(); }
         lds_barrier();
     }
 }
 
+// A job wave's complete state between two time slabs (stored lane-interleaved, 8-B words)
+template <class P>
+struct JobState {
+    P jobs;
+    Runs rn;
+    int pos, pmod;
+};
+template <class P>
+__device__ __forceinline__ void state_io(GLB double* st, JobState<P>& js, int lane, bool save) {
+    constexpr int n = (int)((sizeof(JobState<P>) + 7) / 8);
+    double w[n];
+    if (save) {
+        __builtin_memcpy(w, &js, sizeof(JobState<P>));
+        for (int i = 0; i < n; ++i) st[i * kLanes + lane] = w[i];
+    } else {
+        for (int i = 0; i < n; ++i) w[i] = st[i * kLanes + lane];
+        __builtin_memcpy(&js, w, sizeof(JobState<P>));
+    }
+}
+
 template <class P>
 __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type, int wave, int lane,
-                                      int64_t block) {
+                                      int64_t block, GLB double* stp) {
     LDS Smem& sm = *smp;
     const int64_t asset = block * kLanes + lane;
-    const int nch = (int)((a.T + kChunk - 1) / kChunk);
-    const int64_t nwords = (a.T + 63) / 64;
+    const int c0 = a.c0, nch = a.c1;
+    const int64_t w0 = ((int64_t)c0 * kChunk) >> 6;                     // the slab's first word
+    const int64_t nwords = (a.t1 + 63) / 64 - w0;
     constexpr unsigned S = P::kSer;
     P jobs;
     jobs.init();
@@ -870,6 +915,14 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     rn.C.init(); rn.V.init(); rn.VP.init(); rn.VC.init();
     rn.R.init(); rn.X.init(); rn.Y.init(); rn.XY.init();
     int pos = 0, pmod = 0;      // observations of this lane before the current chunk (and mod kRing)
+    if (stp && a.load_state) {
+        JobState<P> js;
+        state_io(stp, js, lane, false);
+        jobs = js.jobs;
+        rn = js.rn;
+        pos = js.pos;
+        pmod = js.pmod;
+    }
     u64 nb = 0ull, fb = 0ull;   // this wave's NaN / non-finite bits of the current 64-day word
     lds_barrier();              // chunk 0 staged
 #ifdef AFM_FP_PROFILE
@@ -878,7 +931,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     long long twait = 0;
 #endif
 
-    for (int ch = 0; ch < nch; ++ch) {
+    for (int ch = c0; ch < nch; ++ch) {
         const int sh = (ch * kChunk) & 63;                 // chunk offset inside its word
         const u64 cb = (u64)(unsigned)sm.cbyte[ch & 1][lane];
         const bool clean = __builtin_amdgcn_ballot_w64(sm.okbyte[ch & 1][lane] == 0) == 0ull;
@@ -956,8 +1009,8 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
             }
             lds_barrier();
             if (wave == 0) {
-                const int64_t o = ((int64_t)type * nwords + ((int64_t)(ch * kChunk) >> 6)) * a.lda
-                                  + asset;
+                const int64_t o = ((int64_t)type * nwords + (((int64_t)(ch * kChunk) >> 6) - w0))
+                                  * a.lda + asset;
                 a.nanpart[o] = sm.nanmask[lane];
                 a.badpart[o] = sm.badmask[lane];
             }
@@ -972,6 +1025,14 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
         lds_barrier();
 #endif
     }
+    if (stp) {
+        JobState<P> js;
+        js.jobs = jobs;
+        js.rn = rn;
+        js.pos = pos;
+        js.pmod = pmod;
+        state_io(stp, js, lane, true);
+    }
 #ifdef AFM_FP_PROFILE
     if (lane == 0) {
         const long long tot = __builtin_readcyclecounter() - tstart;
@@ -985,6 +1046,15 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     }
 #endif
 }
+
+// words of one wave's slab-carry state (the largest job set's JobState, or a loader's ring)
+template <class P> constexpr int state_words() { return (int)((sizeof(JobState<P>) + 7) / 8); }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+constexpr int kStateWords = cmax(cmax(cmax(cmax(state_words<W0>(), state_words<W1>()),
+    cmax(state_words<W2>(), state_words<W3>())), cmax(cmax(state_words<W4>(), state_words<W5>()),
+    cmax(state_words<W6>(), state_words<W7>()))), cmax(cmax(cmax(state_words<W8>(),
+    state_words<W9>()), cmax(state_words<W10>(), state_words<W11>())), cmax(cmax(
+    state_words<W12>(), state_words<W13>()), cmax(state_words<W14>(), 2 * kRing + 2))));
 
 // TYPES workgroups per block, each with J = 15 / TYPES job waves (job sets W[J*type + wave]) and
 // a loader wave.  PAIR: one workgroup runs TWO such items (two rings, 2 x (J + 1) waves), items
@@ -1029,35 +1099,39 @@ void factor_panel_kernel(Args a) {
     const int ltid = (int)threadIdx.x - half * (J + 1) * kLanes;
     if (ltid < 128) sm->rtab[ltid] = 1.0 / (double)ltid;
     // (the loader's first barrier also publishes rtab)
-    if (wave == J) { load_wave(a, sm, lane, block); return; }
+    // this wave's slab-carry state slot
+    GLB double* stp = a.state ? a.state + (((block * TYPES + type) * (J + 1) + wave) *
+                                           (int64_t)kStateWords * kLanes) : nullptr;
+    if (wave == J) { load_wave(a, sm, lane, block, stp); return; }
     // this type's partial-mask planes (keeps the type out of the job waves' registers)
     Args at = a;
-    const int64_t po = (int64_t)type * ((a.T + 63) / 64) * a.lda;
+    const int64_t w0 = ((int64_t)a.c0 * kChunk) >> 6;
+    const int64_t po = (int64_t)type * ((a.t1 + 63) / 64 - w0) * a.lda;
     at.nanpart = a.nanpart + po;
     at.badpart = a.badpart + po;
 #ifdef AFM_FP_PROFILE
     at.pslot = (int)(block * TYPES + type);          // profile slot of this item
 #endif
 #ifdef AFM_FP_ONLY
-    run_wave<AFM_FP_ONLY>(at, sm, 0, wave, lane, block);
+    run_wave<AFM_FP_ONLY>(at, sm, 0, wave, lane, block, stp);
     return;
 #endif
     switch (type * J + wave) {
-        case 0: run_wave<W0>(at, sm, 0, wave, lane, block); break;
-        case 1: run_wave<W1>(at, sm, 0, wave, lane, block); break;
-        case 2: run_wave<W2>(at, sm, 0, wave, lane, block); break;
-        case 3: run_wave<W3>(at, sm, 0, wave, lane, block); break;
-        case 4: run_wave<W4>(at, sm, 0, wave, lane, block); break;
-        case 5: run_wave<W5>(at, sm, 0, wave, lane, block); break;
-        case 6: run_wave<W6>(at, sm, 0, wave, lane, block); break;
-        case 7: run_wave<W7>(at, sm, 0, wave, lane, block); break;
-        case 8: run_wave<W8>(at, sm, 0, wave, lane, block); break;
-        case 9: run_wave<W9>(at, sm, 0, wave, lane, block); break;
-        case 10: run_wave<W10>(at, sm, 0, wave, lane, block); break;
-        case 11: run_wave<W11>(at, sm, 0, wave, lane, block); break;
-        case 12: run_wave<W12>(at, sm, 0, wave, lane, block); break;
-        case 13: run_wave<W13>(at, sm, 0, wave, lane, block); break;
-        default: run_wave<W14>(at, sm, 0, wave, lane, block); break;
+        case 0: run_wave<W0>(at, sm, 0, wave, lane, block, stp); break;
+        case 1: run_wave<W1>(at, sm, 0, wave, lane, block, stp); break;
+        case 2: run_wave<W2>(at, sm, 0, wave, lane, block, stp); break;
+        case 3: run_wave<W3>(at, sm, 0, wave, lane, block, stp); break;
+        case 4: run_wave<W4>(at, sm, 0, wave, lane, block, stp); break;
+        case 5: run_wave<W5>(at, sm, 0, wave, lane, block, stp); break;
+        case 6: run_wave<W6>(at, sm, 0, wave, lane, block, stp); break;
+        case 7: run_wave<W7>(at, sm, 0, wave, lane, block, stp); break;
+        case 8: run_wave<W8>(at, sm, 0, wave, lane, block, stp); break;
+        case 9: run_wave<W9>(at, sm, 0, wave, lane, block, stp); break;
+        case 10: run_wave<W10>(at, sm, 0, wave, lane, block, stp); break;
+        case 11: run_wave<W11>(at, sm, 0, wave, lane, block, stp); break;
+        case 12: run_wave<W12>(at, sm, 0, wave, lane, block, stp); break;
+        case 13: run_wave<W13>(at, sm, 0, wave, lane, block, stp); break;
+        default: run_wave<W14>(at, sm, 0, wave, lane, block, stp); break;
     }
 }
 
@@ -1143,26 +1217,15 @@ extern "C" int afm_debug_wave_cycles(long long* host, int n) {
 }
 #endif
 
-extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
-                               const double* close, const double* volume, const double* ret1d,
-                               const double* excess, const uint64_t* valid_bits, double* out,
-                               uint64_t* nanfree_bits, uint64_t* finite_bits) {
-    AFM_CTX(ctx);
-    AFM_CHECK_ARG(T > 0 && A > 0, "T and A must be positive");
-    AFM_CHECK_ARG(lda >= A && lda % 64 == 0, "lda must be a multiple of 64 and >= A");
-    AFM_CHECK_ARG(close && volume && valid_bits && out && nanfree_bits, "null buffer");
-    AFM_CHECK_ARG((ret1d == nullptr) == (excess == nullptr),
-                  "ret1d and excess are both given or both NULL");
-    AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
-    const int64_t nwords = (T + 63) / 64;
-    const int64_t nblk = (A + 63) / 64;
-    // workgroups per block: the most job-set splits whose workgroups are all resident at once.
-    // A CU holds two 78-KB rings; the split variants (6, 4 or 2 waves) fit two workgroups per CU,
-    // the unsplit one (16 waves) only one.
+// workgroups per block: the most job-set splits whose workgroups are all resident at once.
+// A CU holds two 78-KB rings; the split variants (6, 4 or 2 waves) fit two workgroups per CU,
+// the unsplit one (16 waves) only one.  3 at least: the unsplit 16-wave workgroup caps the waves
+// at 128 VGPRs, below what the job waves need for the fast step; extra 3-way workgroups simply
+// queue for a free CU slot.
+static int factor_types(afm_ctx* ctx, int64_t nblk) {
     int ncu = 256;
-    AFM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-    // 3 at least: the unsplit 16-wave workgroup caps the waves at 128 VGPRs, below what the job
-    // waves need for the fast step; extra 3-way workgroups simply queue for a free CU slot
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+        ncu = 256;
     int types = 3;
     for (int t : {5, 15})
         if (nblk * t <= 2 * (int64_t)ncu) types = t;
@@ -1170,23 +1233,41 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
         const int t = atoi(e);
         if (t == 1 || t == 3 || t == 5 || t == 15) types = t;
     }
+    return types;
+}
+
+// The factor kernel over the time slab [t0, t1) of the [T]-date series (t0 a multiple of 64;
+// [0, T) = the whole series).  out / nanfree / finite hold the slab's dates only.  state: the
+// carry between consecutive slabs (null for a whole series).
+static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0, int64_t t1,
+                        const double* close, const double* volume, const double* ret1d,
+                        const double* excess, const uint64_t* valid_bits, double* out,
+                        uint64_t* nanfree_bits, uint64_t* finite_bits, double* state) {
+    const int64_t nwords = (t1 - t0 + 63) / 64;                   // the slab's mask words
+    const int64_t nblk = (A + 63) / 64;
+    const int types = factor_types(ctx, nblk);
     uint64_t* part = nullptr;
     AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * types * nwords * lda,
                            ctx->stream));
     afm::Args a;
     a.T = T;
     a.lda = lda;
-    a.plane = T * lda;
+    a.plane = (t1 - t0) * lda;
     a.close = (const GLB double*)close;
     a.volume = (const GLB double*)volume;
     a.vbits = (const GLB uint64_t*)valid_bits;
-    a.out = (GLB double*)out;
+    a.out = (GLB double*)(out - t0 * lda);        // date t's row at a.out + t * lda
     a.nanpart = (GLB uint64_t*)part;
     a.badpart = (GLB uint64_t*)(part + types * nwords * lda);
     a.types = types;
     a.nblk = (int)nblk;
     a.pslot = 0;
     a.fast = 1;
+    a.c0 = (int)(t0 / afm::kChunk);
+    a.c1 = (int)((t1 + afm::kChunk - 1) / afm::kChunk);
+    a.t1 = t1;
+    a.state = (GLB double*)state;
+    a.load_state = t0 > 0 ? 1 : 0;
     // paired 12-wave workgroups for the 3-way split (see factor_panel_kernel); AFM_FP_PAIR=0: A/B
     bool pair = true;
     if (const char* e = getenv("AFM_FP_PAIR")) pair = atoi(e) != 0;
@@ -1230,17 +1311,59 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
     // columns past A (lda padding) carry no presence: their mask words come from valid_bits
     // (zero there), and the factor kernel never ran on blocks past ceil(A/64)
     hipLaunchKernelGGL(afm::masks_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0,
-                       ctx->stream, nwords, lda, types, valid_bits, part, part + types * nw,
-                       nanfree_bits, finite_bits);
+                       ctx->stream, nwords, lda, types, valid_bits + (t0 / 64) * lda, part,
+                       part + types * nw, nanfree_bits, finite_bits);
     AFM_HIP(hipGetLastError());
     if (excess) {                  // NULL: the caller runs afm_labels_f64 (e.g. on another stream)
-        dim3 g2((unsigned)(lda / 64), (unsigned)((T + 3) / 4));
-        hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, (int64_t)0, T,
-                           lda, excess, ret1d, valid_bits, out + 96 * a.plane, out + 97 * a.plane);
+        dim3 g2((unsigned)(lda / 64), (unsigned)((t1 - t0 + 3) / 4));
+        hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, t0, t1, lda,
+                           excess, ret1d, valid_bits, out + 96 * a.plane - t0 * lda,
+                           out + 97 * a.plane - t0 * lda);
         AFM_HIP(hipGetLastError());
     }
     AFM_HIP(hipFreeAsync(part, ctx->stream));
     return AFM_OK;
+}
+
+extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
+                               const double* close, const double* volume, const double* ret1d,
+                               const double* excess, const uint64_t* valid_bits, double* out,
+                               uint64_t* nanfree_bits, uint64_t* finite_bits) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && A > 0, "T and A must be positive");
+    AFM_CHECK_ARG(lda >= A && lda % 64 == 0, "lda must be a multiple of 64 and >= A");
+    AFM_CHECK_ARG(close && volume && valid_bits && out && nanfree_bits, "null buffer");
+    AFM_CHECK_ARG((ret1d == nullptr) == (excess == nullptr),
+                  "ret1d and excess are both given or both NULL");
+    AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
+    return factors_slab(ctx, T, A, lda, 0, T, close, volume, ret1d, excess, valid_bits, out,
+                        nanfree_bits, finite_bits, nullptr);
+}
+
+extern "C" int64_t afm_factors_state_bytes(afm_ctx* ctx, int64_t A) {
+    if (!ctx || A <= 0) return -1;
+    const int64_t nblk = (A + 63) / 64;
+    const int types = factor_types(ctx, nblk);
+    return nblk * types * (afm::kJobSets / types + 1) * (int64_t)afm::kStateWords * 64 * 8;
+}
+
+extern "C" int afm_factors_slab_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,
+                                    int64_t t1, const double* close, const double* volume,
+                                    const double* ret1d, const double* excess,
+                                    const uint64_t* valid_bits, double* out,
+                                    uint64_t* nanfree_bits, uint64_t* finite_bits, double* state) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && A > 0, "T and A must be positive");
+    AFM_CHECK_ARG(lda >= A && lda % 64 == 0, "lda must be a multiple of 64 and >= A");
+    AFM_CHECK_ARG(close && volume && valid_bits && out && nanfree_bits, "null buffer");
+    AFM_CHECK_ARG((ret1d == nullptr) == (excess == nullptr),
+                  "ret1d and excess are both given or both NULL");
+    AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
+    AFM_CHECK_ARG(0 <= t0 && t0 < t1 && t1 <= T && t0 % 64 == 0,
+                  "need 0 <= t0 < t1 <= T with t0 a multiple of 64");
+    AFM_CHECK_ARG(state != nullptr, "the slab state buffer is required");
+    return factors_slab(ctx, T, A, lda, t0, t1, close, volume, ret1d, excess, valid_bits, out,
+                        nanfree_bits, finite_bits, state);
 }
 
 extern "C" int afm_labels_f64(afm_ctx* ctx, int64_t T, int64_t lda, int64_t t0, int64_t t1,

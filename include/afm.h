@@ -60,6 +60,19 @@ int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
                     const double* close, const double* volume, const double* ret1d,
                     const double* excess, const uint64_t* valid_bits,
                     double* out, uint64_t* nanfree_bits, uint64_t* finite_bits);
+/* The same panel one TIME SLAB at a time (series longer than one GPU's HBM holds as output,
+ * BASELINE config D): dates [t0, t1) of the [T]-date inputs, t0 a multiple of 64, called for
+ * consecutive slabs from t0 = 0.  out [AFM_N_FACTORS][t1 - t0][lda], nanfree_bits / finite_bits
+ * [ceil((t1 - t0)/64)][lda] hold the slab's dates only.  state: a device buffer of
+ * afm_factors_state_bytes(ctx, A) bytes carrying every recurrence state and the observation
+ * rings from one slab to the next; the concatenated slabs equal one afm_factors_f64 call bit for
+ * bit. */
+int64_t afm_factors_state_bytes(afm_ctx* ctx, int64_t A);
+int afm_factors_slab_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,
+                         int64_t t1, const double* close, const double* volume,
+                         const double* ret1d, const double* excess, const uint64_t* valid_bits,
+                         double* out, uint64_t* nanfree_bits, uint64_t* finite_bits,
+                         double* state);
 
 /* out_bits = in_bits without each asset's last present day (valid_bits): the rows whose
  * shift(-1) labels are NaN.  Used to mask the regression rows up front (the Gram's REDO pass

@@ -73,3 +73,32 @@ def test_group_sizing():
     assert group_blocks(g, budget_bytes=10**15) == 47                  # everything in one
     b = group_blocks(g, budget_bytes=21 * per_blk + 2 * 8 * 10 * 64 * 21)
     assert b <= 21 and ((47 + b - 1) // b) == 3 and b == 16            # 16, 16, 15
+
+
+@pytest.mark.parametrize("types,step", [(15, 64), (5, 320), (3, 1024), (3, 704)])
+def test_time_slabs_identical_to_one_launch(monkeypatch, types, step):
+    """Config D's default build: ALL assets over consecutive time slabs, every recurrence state
+    and observation ring carried across slab boundaries in the state buffer -- the concatenated
+    slabs (98 planes incl. the labels, nanfree bits) equal one launch bit for bit, for every
+    workgroup split of the job sets (3 = the paired 12-wave launch)."""
+    import torch
+    import afm
+    from afm.intraday import factor_panel_slabs, make_panel_device
+    torch.cuda.set_device(0)
+    monkeypatch.setenv("AFM_FP_TYPES", str(types))
+    g = make_panel_device(300, 2500, seed=9, hole_frac=0.01)
+    full, nf_full = afm.factor_panel(g)
+    vb = afm.unpack_bits(g.vbits, g.T)
+    seen = []
+
+    def consume(t0, t1, out, nanfree):
+        m = vb[t0:t1]
+        a, b = out[:, m], full[:, t0:t1][:, m]
+        assert torch.equal(torch.isnan(a), torch.isnan(b)), (t0, t1)
+        assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b)), (t0, t1)
+        w0, w1 = t0 // 64, (t1 + 63) // 64
+        assert torch.equal(nanfree, nf_full[w0:w1]), (t0, t1)
+        seen.append((t0, t1))
+
+    n = factor_panel_slabs(g, consume, bars_per_slab=step)
+    assert n == (g.T + step - 1) // step and seen[-1][1] == g.T

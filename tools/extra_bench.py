@@ -170,20 +170,31 @@ def bench_talib(reps, A=10000, T=5040):
 
 
 def bench_intraday(reps, A=3000, T=2 * 252 * 390):
+    """Config D both ways: time slabs over all assets (the default build, state carried across
+    slabs) and asset groups over the whole series."""
     import torch
-    from afm.intraday import factor_panel_groups, group_blocks, make_panel_device
+    from afm.intraday import (factor_panel_groups, factor_panel_slabs, group_blocks,
+                              make_panel_device, slab_bars)
     g = make_panel_device(A, T, seed=2023)
     bars = int(g.valid.sum().item())
+    byts = 816 * bars
+    step = slab_bars(g)
+    slabs = []
+    factor_panel_slabs(g, lambda t0, t1, o, nf: slabs.append((t0, t1)), step)   # warm-up
+    ms_s = timed(lambda: factor_panel_slabs(g, lambda *x: None, step), max(1, reps // 3))
     bpg = group_blocks(g)
     groups = []
     factor_panel_groups(g, lambda a0, a1, o, nf: groups.append((a0, a1)), bpg)   # warm-up
-    ms = timed(lambda: factor_panel_groups(g, lambda *x: None, bpg), max(1, reps // 3))
-    byts = 816 * bars
+    ms_g = timed(lambda: factor_panel_groups(g, lambda *x: None, bpg), max(1, reps // 3))
     return {"stage": "intraday", "workload": f"config D: {A} assets x {T} 1-minute bars "
-                                             f"({bars} present asset-bars), 98 factors, "
-                                             f"{len(groups)} asset groups of {bpg} blocks",
-            "ms": round(ms, 1), "asset_bars_per_s": round(bars / (ms * 1e-3), 1),
-            "algorithmic_GB": round(byts / 1e9, 1), "GBps": round(byts / (ms * 1e-3) / 1e9, 1)}
+                                             f"({bars} present asset-bars), 98 factors",
+            "slabs": {"n": len(slabs), "bars_per_slab": step, "ms": round(ms_s, 1),
+                      "asset_bars_per_s": round(bars / (ms_s * 1e-3), 1),
+                      "GBps": round(byts / (ms_s * 1e-3) / 1e9, 1)},
+            "groups": {"n": len(groups), "blocks_per_group": bpg, "ms": round(ms_g, 1),
+                       "asset_bars_per_s": round(bars / (ms_g * 1e-3), 1),
+                       "GBps": round(byts / (ms_g * 1e-3) / 1e9, 1)},
+            "algorithmic_GB": round(byts / 1e9, 1)}
 
 
 def main():
