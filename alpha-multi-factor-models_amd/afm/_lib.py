@@ -57,6 +57,7 @@ SIGNATURES = {
     "afm_xs_prepare_f64": (I32, [P, I64, I64, I64, P, P, P, P, P, P]),
     "afm_xs_prepare_range_f64": (I32, [P, I64, I64, I64, I64, I64, P, P, P, P, P, P]),
     "afm_xs_rank_f64": (I32, [P, I64, I64, P, P, P, P, P, P]),
+    "afm_xs_layers_f64": (I32, [P, I64, I64, P, P, P, P, P, P]),
     "afm_xs_stats_f64": (I32, [P, I64, I64, P, I64, P, P, P, P, I32, P, P, P, P]),
     "afm_xs_series_f64": (I32, [P, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
     "afm_zscore_stats_f64": (I32, [P, P, I64, I64, I64, P, I32, P, I64, I64, P, P]),

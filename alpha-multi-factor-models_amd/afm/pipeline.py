@@ -624,9 +624,9 @@ class Pipeline:
             chk(L.afm_xs_prepare_range_f64(h, Ta, full.A, lda, d0, d1, P(self.pred[a0:]),
                                            P(an["fr"]), P(an["scratch"]), P(an["rows"]),
                                            P(an["rows_idx"]), P(an["nrows"])), "xs_prepare")
-            chk(L.afm_xs_rank_f64(h, d1 - d0, lda, P(an["rows"][0, d0:]), P(an["nrows"][d0:]),
-                                  P(an["skey"][d0:]), P(an["sidx"][d0:]), P(an["ra"][d0:]),
-                                  P(an["rd"][d0:])), "xs_rank")
+            chk(L.afm_xs_layers_f64(h, d1 - d0, lda, P(an["rows"][0, d0:]), P(an["nrows"][d0:]),
+                                    P(an["skey"][d0:]), P(an["sidx"][d0:]), P(an["ra"][d0:]),
+                                    P(an["rd"][d0:])), "xs_layers")
             chk(L.afm_xs_stats_f64(h, Ta, lda, P(self.an_dates[j0:]), j1 - j0, P(an["rows"]),
                                    P(an["nrows"]), P(an["ra"]), P(an["rd"]), 10, P(an["ic"][j0:]),
                                    P(an["layer_mean"][j0:]), P(an["layer_cnt"][j0:]),

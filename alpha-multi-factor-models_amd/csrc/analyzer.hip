@@ -457,6 +457,243 @@ __global__ __launch_bounds__(kWT) void xs_rank_kernel(RankArgs g, int lds_rows) 
     }
 }
 
+// ---- A3/A4 without a sort: the decile layer and the top-10 of every row --------------------
+// xs_stats needs of the ranks only (a) each row's layer = min(int(rank/n*10)+1, 10) (KKT:328-330)
+// and (b) the rows of descending rank <= 10 with that rank (KKT:359-369).  The layer is monotone
+// in the rank, so with R_l = the largest rank of layer <= l, layer(e) = 1 + #{l < 10 : (key_e, e)
+// > the R_l-th smallest (key, position)}: nine order statistics, found by one radix select that
+// narrows all nine prefixes in the same passes over register-resident keys, exact ties resolved
+// by position.  The top 10 (key descending, position ascending) by the same select.  Outputs in
+// xs_rank's convention for xs_stats: rank_asc = the first rank of the row's layer (xs_stats
+// recomputes the same layer from it), rank_desc = the true rank of a top-10 row, n + 1 else.
+constexpr int kLT = 512;                  // threads
+constexpr int kLR = 24;                   // register keys per thread: n <= 12288
+constexpr int kNTg = 10;                  // targets: 9 decile bounds + the 10th largest
+
+struct LayerSmem {
+    int hist[kNTg][256];
+    u64 prefix[kNTg];
+    int need[kNTg];
+    int eqtot[kNTg];
+    int rneed[kNTg];                      // target rank (1-based), 0 = no row
+    int eqidx[kNTg];                      // the position of the target row
+    int ntop;
+    u64 topk[kTopK];
+    int topi[kTopK];
+};
+
+__device__ __forceinline__ int layer_of(int r, int n) {
+    int l = (int)((double)r / (double)n * kLayers) + 1;
+    return l > kLayers ? kLayers : l;
+}
+
+__global__ __launch_bounds__(kLT) void xs_layers_kernel(RankArgs g) {
+    __shared__ LayerSmem sh;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t t = blockIdx.x;
+    const int n = g.nrows[t];
+    const int64_t base = t * g.lda;
+    if (n <= 0) return;
+    // keys: ascending order key; the top-10 target runs on the complemented key (descending)
+    u64 ks[kLR];
+#pragma unroll
+    for (int j = 0; j < kLR; ++j) {
+        const int e = j * kLT + tid;
+        ks[j] = e < n ? okey(g.rows[base + e]) : 0ull;
+    }
+    if (tid < kNTg) {
+        int r;
+        if (tid < kNTg - 1) {             // R_l: the largest rank with layer <= l (l = tid + 1)
+            int lo = 0, hi = n;           // f(lo) <= l (f(0) := 0), f(hi + 1) > l or hi = n
+            while (lo < hi) {
+                const int m = (lo + hi + 1) >> 1;
+                if (layer_of(m, n) <= tid + 1) lo = m; else hi = m - 1;
+            }
+            r = lo;
+        } else {
+            r = n >= kTopK ? kTopK : n;   // the 10th largest (or the n-th)
+        }
+        sh.rneed[tid] = r;
+        sh.need[tid] = r;
+        sh.prefix[tid] = 0ull;
+        sh.eqidx[tid] = 0;
+    }
+    __syncthreads();
+    u64 pmask = 0ull;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        for (int e = tid; e < kNTg * 256; e += kLT) (&sh.hist[0][0])[e] = 0;
+        __syncthreads();
+        if (shift == 56) {
+            // every target's prefix is empty: one histogram of the top digit, copied to the
+            // ascending targets and mirrored for the complemented one
+#pragma unroll
+            for (int j = 0; j < kLR; ++j)
+                if (j * kLT + tid < n) atomicAdd(&sh.hist[0][ks[j] >> 56], 1);
+            __syncthreads();
+            if (tid < 256) {
+                const int h = sh.hist[0][tid];
+#pragma unroll
+                for (int q = 1; q < kNTg - 1; ++q) sh.hist[q][tid] = h;
+                sh.hist[kNTg - 1][255 - tid] = h;
+            }
+        } else {
+            u64 pf[kNTg];
+            bool act[kNTg];
+#pragma unroll
+            for (int q = 0; q < kNTg; ++q) {
+                pf[q] = sh.prefix[q];
+                act[q] = sh.need[q] > 0;
+            }
+#pragma unroll
+            for (int j = 0; j < kLR; ++j) {
+                if (j * kLT + tid < n) {
+#pragma unroll
+                    for (int q = 0; q < kNTg; ++q) {
+                        const u64 kk = q < kNTg - 1 ? ks[j] : ~ks[j];
+                        if (act[q] && (kk & pmask) == pf[q])
+                            atomicAdd(&sh.hist[q][(kk >> shift) & 255], 1);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // digit pick, target q on wave q % 4: the smallest digit d with cumulative count >= need
+        for (int q = tid >> 6; q < kNTg; q += kLT / 64) {
+            const int nd = sh.need[q];
+            if (nd > 0) {
+                const int h0 = sh.hist[q][4 * lane], h1 = sh.hist[q][4 * lane + 1],
+                          h2 = sh.hist[q][4 * lane + 2], h3 = sh.hist[q][4 * lane + 3];
+                const int s4 = h0 + h1 + h2 + h3;
+                int P = s4;                                // inclusive prefix over lanes
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(P, o, 64);
+                    if (lane >= o) P += v;
+                }
+                const u64 m = __ballot(P >= nd);
+                const int L = __builtin_ctzll(m);
+                if (lane == L) {
+                    int acc = P - s4, d = 4 * L, hd = h0;
+                    if (acc + h0 >= nd) { d = 4 * L; hd = h0; }
+                    else if (acc + h0 + h1 >= nd) { d = 4 * L + 1; hd = h1; acc += h0; }
+                    else if (acc + h0 + h1 + h2 >= nd) { d = 4 * L + 2; hd = h2; acc += h0 + h1; }
+                    else { d = 4 * L + 3; hd = h3; acc += h0 + h1 + h2; }
+                    sh.prefix[q] |= (u64)d << shift;
+                    sh.need[q] = nd - acc;
+                    sh.eqtot[q] = hd;
+                }
+            }
+        }
+        pmask |= 255ull << shift;
+        __syncthreads();
+    }
+    // ties at each target's key: the need-th smallest position among them, by the same select
+    // over the positions (14 bits: two passes of 7)
+    {
+        int epfx[kNTg];
+#pragma unroll
+        for (int q = 0; q < kNTg; ++q) epfx[q] = 0;
+        int emask = 0;
+        for (int shift = 7; shift >= 0; shift -= 7) {
+            for (int e = tid; e < kNTg * 256; e += kLT) (&sh.hist[0][0])[e] = 0;
+            u64 pf[kNTg];
+            bool act[kNTg];
+#pragma unroll
+            for (int q = 0; q < kNTg; ++q) {
+                pf[q] = sh.prefix[q];
+                act[q] = sh.need[q] > 0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kLR; ++j) {
+                const int e = j * kLT + tid;
+                if (e < n) {
+#pragma unroll
+                    for (int q = 0; q < kNTg; ++q) {
+                        const u64 kk = q < kNTg - 1 ? ks[j] : ~ks[j];
+                        if (act[q] && kk == pf[q] && (e & emask) == epfx[q])
+                            atomicAdd(&sh.hist[q][(e >> shift) & 127], 1);
+                    }
+                }
+            }
+            __syncthreads();
+            for (int q = tid >> 6; q < kNTg; q += kLT / 64) {
+                const int nd = sh.need[q];
+                if (nd > 0) {
+                    const int h0 = sh.hist[q][2 * lane], h1 = sh.hist[q][2 * lane + 1];
+                    const int s2 = h0 + h1;
+                    int P = s2;
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int v = __shfl_up(P, o, 64);
+                        if (lane >= o) P += v;
+                    }
+                    const u64 m = __ballot(P >= nd);
+                    const int L = __builtin_ctzll(m);
+                    if (lane == L) {
+                        const int acc = P - s2;
+                        const int d = acc + h0 >= nd ? 2 * L : 2 * L + 1;
+                        sh.eqidx[q] = (shift == 7 ? 0 : sh.eqidx[q]) | (d << shift);
+                        sh.need[q] = nd - (acc + h0 >= nd ? acc : acc + h0);
+                    }
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < kNTg; ++q) epfx[q] = sh.need[q] > 0 ? sh.eqidx[q] : 0;
+            emask |= 127 << shift;
+            __syncthreads();
+        }
+    }
+    // layers; the top-10 rows (keys >= the 10th largest in (key desc, position asc) order)
+    u64 kq[kNTg];
+    int iq[kNTg];
+    bool has[kNTg];
+#pragma unroll
+    for (int q = 0; q < kNTg; ++q) {
+        kq[q] = sh.prefix[q];
+        iq[q] = sh.eqidx[q];
+        has[q] = sh.rneed[q] > 0;
+    }
+    int r0[kLayers];                                  // first rank of each layer
+    r0[0] = 1;
+#pragma unroll
+    for (int l = 1; l < kLayers; ++l) r0[l] = sh.rneed[l - 1] + 1;
+    if (tid == 0) sh.ntop = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kLR; ++j) {
+        const int e = j * kLT + tid;
+        if (e < n) {
+            int l = 0;
+#pragma unroll
+            for (int q = 0; q < kNTg - 1; ++q)
+                l += !has[q] || ks[j] > kq[q] || (ks[j] == kq[q] && e > iq[q]) ? 1 : 0;
+            int rl = r0[0];
+#pragma unroll
+            for (int q = 1; q < kLayers; ++q) rl = l == q ? r0[q] : rl;
+            g.rank_asc[base + e] = rl;
+            const u64 kd = ~ks[j];                    // descending order key
+            const int q = kNTg - 1;
+            const bool top = kd < kq[q] || (kd == kq[q] && e <= iq[q]);
+            g.rank_desc[base + e] = n + 1;
+            if (top) {
+                const int s = atomicAdd(&sh.ntop, 1);
+                sh.topk[s] = kd;
+                sh.topi[s] = e;
+            }
+        }
+    }
+    __syncthreads();
+    const int ntop = sh.ntop;
+    if (tid < ntop) {                                 // rank among the top rows by counting
+        const u64 mk = sh.topk[tid];
+        const int mi = sh.topi[tid];
+        int rk = 1;
+        for (int f = 0; f < ntop; ++f)
+            rk += sh.topk[f] < mk || (sh.topk[f] == mk && sh.topi[f] < mi);
+        g.rank_desc[base + mi] = rk;
+    }
+}
+
 // ---- A2-A4: per (date, return type) sequential statistics --------------------------------------
 struct StatArgs {
     int64_t T, lda;
@@ -860,6 +1097,20 @@ extern "C" int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const doubl
     }
     hipLaunchKernelGGL(xs_rank_kernel, dim3((unsigned)T), dim3(kWT), lds, ctx->stream, g,
                        lds_rows);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_xs_layers_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* rows,
+                                 const int32_t* nrows, uint64_t* skey, int32_t* sidx,
+                                 int32_t* rank_asc, int32_t* rank_desc) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && lda % 64 == 0, "bad shape");
+    AFM_CHECK_ARG(rows && nrows && skey && sidx && rank_asc && rank_desc, "null buffer");
+    if (lda > (int64_t)kLR * kLT)                  // wider dates: the sorting kernel
+        return afm_xs_rank_f64(ctx, T, lda, rows, nrows, skey, sidx, rank_asc, rank_desc);
+    RankArgs g{T, lda, rows, nrows, (u64*)skey, sidx, rank_asc, rank_desc};
+    hipLaunchKernelGGL(xs_layers_kernel, dim3((unsigned)T), dim3(kLT), 0, ctx->stream, g);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

@@ -234,6 +234,12 @@ int afm_xs_prepare_range_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, in
 int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* rows,
                     const int32_t* nrows, uint64_t* skey, int32_t* sidx, int32_t* rank_asc,
                     int32_t* rank_desc);
+/* What afm_xs_stats_f64 reads of the ranks, without sorting (KKT:328-330, 359-369): rank_asc =
+ * the first rank of the row's decile layer, rank_desc = the exact descending rank of the rows
+ * ranked 1..10, nrows + 1 for the rest.  Same arguments as afm_xs_rank_f64 (lda > 12288: it). */
+int afm_xs_layers_f64(afm_ctx* ctx, int64_t T, int64_t lda, const double* rows,
+                      const int32_t* nrows, uint64_t* skey, int32_t* sidx, int32_t* rank_asc,
+                      int32_t* rank_desc);
 /* For the nd dates (DEVICE int32 grid indices): IC [nd][3] (nancorr Welford, KKT:344-345),
  * decile layer means [nd][3][10] and counts [nd][10] (KKT:328-332), top-10 factor-weighted
  * returns port [nd][3] (KKT:359-369; mcols = pivot columns present, <= 10). */

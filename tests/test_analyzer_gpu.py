@@ -68,3 +68,49 @@ def test_analyzer_large_panel_vs_oracle():
         assert same(an.layered_ret_dfs[rt][rt].values, o[f"lay_{rt}"])
         assert same(an.ls_ret_dfs[rt][rt].values, o[f"ls_{rt}"])
     assert same(an.port_ret_df["Returns"].values, o["pt_ret"])
+
+
+@pytest.mark.parametrize("lda,kind", [(64, "normal"), (1024, "ties"), (12288, "normal"),
+                                      (12288, "ties"), (12352, "normal")])
+def test_layers_match_exact_ranks(lda, kind):
+    """afm_xs_layers_f64 (no sort) gives xs_stats exactly what it reads of afm_xs_rank_f64's ranks:
+    each row's decile layer (KKT:328-330) and the descending ranks 1..10 (KKT:359-369), with
+    method='first' ties; row counts 0, 1, 9, 10, 11, ... up to the register capacity (12288) and
+    past it (the sorting fallback)."""
+    import torch
+    from afm import _lib
+    rng = np.random.default_rng(lda)
+    T = 40
+    counts = np.concatenate([[0, 1, 2, 9, 10, 11, 19, 20, 21, lda],
+                             rng.integers(0, lda + 1, T - 10)]).astype(np.int32)
+    if kind == "ties":
+        v = rng.integers(-3, 4, (T, lda)).astype(np.float64) * 0.25
+        v[::3] = 1.5                                       # all-equal dates
+        v[1::7, ::5] = -0.0                                # signed zeros tie with 0
+    else:
+        v = rng.normal(size=(T, lda))
+    dev = torch.device("cuda", 0)
+    rows = torch.from_numpy(v).to(dev)
+    nrows = torch.from_numpy(counts).to(dev)
+    L, P, h = _lib.lib(), _lib.ptr, _lib.Context.get(0).bind_stream()
+    out = []
+    for fn in (L.afm_xs_rank_f64, L.afm_xs_layers_f64):
+        skey = torch.empty((T, lda), dtype=torch.int64, device=dev)
+        sidx = torch.empty((T, lda), dtype=torch.int32, device=dev)
+        ra = torch.full((T, lda), -1, dtype=torch.int32, device=dev)
+        rd = torch.full((T, lda), -1, dtype=torch.int32, device=dev)
+        _lib.check(fn(h, T, lda, P(rows), P(nrows), P(skey), P(sidx), P(ra), P(rd)), "rank")
+        out.append((ra.cpu().numpy(), rd.cpu().numpy()))
+    (ra0, rd0), (ra1, rd1) = out
+    for t in range(T):
+        n = int(counts[t])
+        if n == 0:
+            continue
+        lay0 = np.minimum((ra0[t, :n] / n * 10).astype(int) + 1, 10)
+        lay1 = np.minimum((ra1[t, :n] / n * 10).astype(int) + 1, 10)
+        assert np.array_equal(lay0, lay1), t
+        top0 = np.where(rd0[t, :n] <= 10, rd0[t, :n], n + 1)
+        if lda <= 12288:
+            assert np.array_equal(top0, rd1[t, :n]), t
+        else:                                              # the fallback: exact ranks
+            assert np.array_equal(rd0[t, :n], rd1[t, :n]), t

@@ -33,6 +33,9 @@ def main():
         "xs_rank": lambda: L.afm_xs_rank_f64(h, Ta, lda, P(an["rows"]), P(an["nrows"]),
                                              P(an["skey"]), P(an["sidx"]), P(an["ra"]),
                                              P(an["rd"])),
+        "xs_layers": lambda: L.afm_xs_layers_f64(h, Ta, lda, P(an["rows"]), P(an["nrows"]),
+                                                 P(an["skey"]), P(an["sidx"]), P(an["ra"]),
+                                                 P(an["rd"])),
         "xs_stats": lambda: L.afm_xs_stats_f64(h, Ta, lda, P(pipe.an_dates), pipe.an_nd,
                                                P(an["rows"]), P(an["nrows"]), P(an["ra"]),
                                                P(an["rd"]), 10, P(an["ic"]), P(an["layer_mean"]),
