@@ -99,6 +99,7 @@ struct ZGramArgs {
     int nrb;                 // mode 1: row-blocks from blk0
     int nchunk;              // mode 1: date chunks of [t0, t0 + nt)
     double* part;            // mode 0: [nt][nblk][PE]; mode 1: [nrb][nchunk][PE]
+    int even;                // pad every item to an even slot count (zgram_produce_pairs)
 };
 
 // The ring: nslots slots of (p + 4) LDS rows (rows 0..p+1 staged, row p+2 stays zero: the
@@ -127,14 +128,15 @@ __device__ __forceinline__ void signal_count(int* p, int lane) {
 //  mode 0: item = (date d, block b): the block's row-blocks (at least one) at date t0 + d;
 //  mode 1: item = (row-block r, chunk c): row-block r at every date of chunk c (at least one
 //          slot: an empty chunk stages one all-masked block).
+// With g.even every item has an EVEN number of slots (an odd count gets one all-masked slot
+// more): zgram_produce_pairs stages two buffers per loop iteration, never straddling two items.
 // Every wave walks the same sequence; the item's last row-block flushes the consumers.
 struct Seq {
     int item, nitems, stride;
     int t, a_lo;             // current row-block: date, first asset
-    int masked;              // an empty chunk's placeholder slot
-    int k, kend;             // position inside the item (row-block or date)
+    int masked;              // an all-masked slot (empty chunk, or the padding slot)
+    int k, kend, kreal;      // position inside the item (row-block or date); real slots < kreal
     __device__ void start(const ZGramArgs& g) {
-        masked = 0;
         if (g.mode == 0) {
             const int d = item / g.nblk, b = item - d * g.nblk;
             t = (int)g.t0 + d;
@@ -144,17 +146,20 @@ struct Seq {
             const int n = hi > lo ? (hi - lo + 63) / 64 : 0;
             a_lo = lo;
             k = 0;
-            kend = n > 0 ? n : 1;
+            kreal = n;
+            kend = (n > 0 ? n : 1) + (g.even ? ((n > 0 ? n : 1) & 1) : 0);
         } else {
             const int r = item / g.nchunk, c = item - r * g.nchunk;
             const int c0 = (int)g.t0 + (int)(((int64_t)c * g.nt) / g.nchunk);
             const int c1 = (int)g.t0 + (int)(((int64_t)(c + 1) * g.nt) / g.nchunk);
+            const int n = c1 > c0 ? c1 - c0 : 1;
             a_lo = (int)g.blk0 + r * 64;
             k = c0;
-            kend = c1 > c0 ? c1 : c0 + 1;
-            masked = c1 > c0 ? 0 : 1;
+            kreal = c1;
+            kend = c0 + n + (g.even ? (n & 1) : 0);
             t = c0;
         }
+        masked = k >= kreal ? 1 : 0;
     }
     __device__ void init(const ZGramArgs& g) {
         stride = gridDim.x;
@@ -168,8 +173,9 @@ struct Seq {
     __device__ void advance(const ZGramArgs& g) {
         if (k + 1 < kend) {
             ++k;
+            masked = k >= kreal ? 1 : 0;
             if (g.mode == 0) a_lo += 64;
-            else t = k;
+            else t = masked ? t : k;              // a padding slot keeps a real date (masked)
             return;
         }
         item += stride;
@@ -290,6 +296,125 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, con
         if (MODE == 0 && ha) zload(A.zoff);
         hc = cur.valid();
         if (hc) { xload(C); cur.advance(g); }
+    }
+}
+
+// zgram_produce with a prefetch the compiler's waits keep in flight (the per-date FM Grams:
+// their producers are load-latency-bound, 3.9 -> 3.0 ms): every xload / zload issues its loads on
+// every path and the presence word is tested only when staging -- a load consumed where it is
+// issued makes the compiler wait for every outstanding load, the whole prefetch, right there.
+// Items have an even slot count (g.even), so each iteration stages the pair (A, C) of one item.
+// (The pooled Gram keeps zgram_produce: it is bound by the MFMA / staging serialisation on the
+// SIMDs, and there the deeper prefetch measured slower, 11.1 -> 12.1 ms.)
+template <int NT, int MODE, bool ZS, int PW>
+__device__ void zgram_produce_pairs(const ZGramArgs& g, ZSmem& sm, const int lane, const int pw_rt) {
+    // AFM_ZG_TPL: the wave index as a compile-time constant (immediate LDS offsets) or not
+    const int pw = AFM_ZG_TPL ? PW : pw_rt;
+    constexpr int MC = ZCfg<NT>::MC;
+    const int p = g.p;
+    const int K = p + 2;
+    const int lda = (int)g.lda;
+    // plane and zs row of every column (SGPRs); the 64-bit addresses are re-derived at each load
+    // (SALU work -- the asm keeps the compiler from hoisting 2 x MC 64-bit pointers into SGPRs)
+    // (plane | zs row << 16: one SGPR per column)
+    int pk[MC];
+#pragma unroll
+    for (int j = 0; j < MC; ++j) {
+        const int k = pw + kZProd * j;
+        const bool feat = k >= 1 && k <= p;
+        const int pl = feat ? g.cols[k - 1] : g.ycol;
+        const int zr = feat ? (g.zcols ? g.zcols[k - 1] : k - 1) : g.zid;
+        pk[j] = __builtin_amdgcn_readfirstlane(pl | (zr << 16));
+    }
+    auto xsrc = [&](int j) {
+        int q = pk[j];
+        asm volatile("" : "+s"(q));
+        return reinterpret_cast<const char*>(g.base + (int64_t)(q & 0xffff) * g.col_stride);
+    };
+    auto zsrc = [&](int j) {
+        int q = pk[j];
+        asm volatile("" : "+s"(q));
+        return (unsigned)((q >> 16) * lda) * 16u;
+    };
+    const char* zb = reinterpret_cast<const char*>(g.zs);
+    struct Buf {
+        double x[MC];
+        uint32_t word;           // the half presence word holding the row's bit, tested when
+        bool in, valid;          // staging: a load consumed at issue would make the compiler
+        unsigned zoff;           // wait for every outstanding load (the whole prefetch) there
+        int t, item;
+    };
+    Buf A, C;
+    double mu[MC], rs[MC];
+    Seq cur;
+    cur.init(g);
+    // Every xload / zload issues its loads on every path (a finished sequence or a masked slot
+    // reads the first cell): with the same loads in every iteration the compiler's waits before
+    // a stage cover only that buffer, and the younger prefetch stays in flight.
+    auto xload = [&](Buf& B) {
+        const bool v = cur.valid();
+        const int a = cur.row_asset(lane);
+        const bool in = v && !cur.masked && a < (int)g.a_end;
+        const int ac = in ? a : 0, tl = in ? cur.t : 0;
+        B.valid = v;
+        B.in = in;
+        B.t = cur.t;
+        B.item = v ? cur.item : -1;
+        B.zoff = (unsigned)ac * 16u;
+        B.word = reinterpret_cast<const uint32_t*>(g.bits)[((int64_t)(tl >> 6) * lda + ac) * 2 +
+                                                           ((tl >> 5) & 1)];
+#if defined(AFM_ZG_SKIP) && AFM_ZG_SKIP == 2              // experiments: consumers alone
+        B.in = false;
+#else
+        const unsigned off = (unsigned)(tl * lda + ac) * 8u;
+#pragma unroll
+        for (int j = 0; j < MC; ++j) B.x[j] = *reinterpret_cast<const double*>(xsrc(j) + off);
+#endif
+        if (v) cur.advance(g);
+    };
+    auto zload = [&](const unsigned zoff) {
+#if defined(AFM_ZG_SKIP) && AFM_ZG_SKIP == 2
+        return;
+#endif
+        if (!ZS) return;                             // raw columns: no statistics
+#pragma unroll
+        for (int j = 0; j < MC; ++j) {
+            const double2 m = *reinterpret_cast<const double2*>(zb + zsrc(j) + zoff);
+            mu[j] = m.x;
+            rs[j] = m.y;
+        }
+    };
+    int slot = 0, gen = 0;
+    auto stage = [&](const Buf& B) {
+        wait_count(&sm.freed[slot], ZCfg<NT>::NWAIT * gen);
+        lds_double* tb = sm.tile + slot * sm.slot_elems + lane;
+        const bool ok = B.in && ((B.word >> (B.t & 31)) & 1u);
+#pragma unroll
+        for (int j = 0; j < MC; ++j) {
+            const int k = pw + kZProd * j;
+            const int lrow = k < K ? k : p + 3;      // the dump row takes the dummy columns
+            double v = ZS ? (B.x[j] - mu[j]) * rs[j] : B.x[j];   // y: identity row {0, 1}
+            if (k == 0) v = 1.0;                     // the ones column (wave 0, j = 0)
+            tb[lrow * kZRS] = ok ? v : 0.0;
+        }
+        signal_count(&sm.ready[slot], lane);
+        if (++slot == sm.nslots) { slot = 0; ++gen; }
+    };
+    xload(A);
+    if (MODE == 0) zload(A.zoff);
+    xload(C);
+    while (A.valid) {                                // one item per iteration (even slot count)
+        // mode 1: the item keeps its 64 assets -- its statistics stay in registers for its dates
+        if (MODE == 1) zload(A.zoff);
+        const int item = A.item;
+        do {
+            stage(A);
+            if (MODE == 0) zload(C.zoff);            // next statistics first, then x two ahead
+            xload(A);
+            stage(C);
+            if (MODE == 0) zload(A.zoff);
+            xload(C);
+        } while (A.valid && A.item == item);
     }
 }
 
@@ -473,7 +598,9 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
     __syncthreads();
     if (wave >= 4 && wave < 4 + kZProd) {
         if (prio & 1) __builtin_amdgcn_s_setprio(1);
-        if (!AFM_ZG_TPL) {
+        if (NT == 2) {
+            zgram_produce_pairs<NT, MODE, ZS, 0>(g, sm, lane, wave - 4);
+        } else if (!AFM_ZG_TPL) {
             zgram_produce<NT, MODE, ZS, 0>(g, sm, lane, wave - 4);
         } else {
             switch (wave - 4) {
@@ -673,8 +800,10 @@ extern "C" int afm_zgram_f64(afm_ctx* ctx, const double* base, int64_t col_strid
     AFM_CHECK_ARG(nblk >= 1 && blk_assets > 0 && blk_assets % 64 == 0 && nt * nblk < (1ll << 31),
                   "blocks must be 64-aligned");
     if (nt == 0) return AFM_OK;
+    // the two-tile shape (NT = 2) stages item pairs (zgram_produce_pairs): even slot counts
+    const int even = (!zs || zgram_nt(p) == 2) ? 1 : 0;
     ZGramArgs g{base, col_stride, lda, cols, zcols, p, ycol, zid, zs, bits, t0, nt, 0, nblk, blk0,
-                blk_assets, a_end, 0, 1, part};
+                blk_assets, a_end, 0, 1, part, even};
     if (!zs) return launch_zgram<2, 0, false>(ctx, g, nt * nblk, grid);   // FM: raw columns
     return zgram_nt(p) == 2 ? launch_zgram<2, 0, true>(ctx, g, nt * nblk, grid)
                             : launch_zgram<7, 0, true>(ctx, g, nt * nblk, grid);
@@ -691,7 +820,7 @@ extern "C" int afm_zpool_f64(afm_ctx* ctx, const double* base, int64_t col_strid
     AFM_CHECK_ARG(nrb >= 0 && nchunk >= 1 && (int64_t)nrb * nchunk < (1ll << 31), "bad leaves");
     if (nrb == 0) return AFM_OK;
     ZGramArgs g{base, col_stride, lda, cols, zcols, p, ycol, zid, zs, bits, t0, nt, 1, 1, blk0,
-                64, a_end, nrb, nchunk, part};
+                64, a_end, nrb, nchunk, part, zgram_nt(p) == 2 ? 1 : 0};
     AFM_CHECK_ARG(zs != nullptr, "afm_zpool_f64 needs zs");
     return zgram_nt(p) == 2 ? launch_zgram<2, 1, true>(ctx, g, (int64_t)nrb * nchunk, grid)
                             : launch_zgram<7, 1, true>(ctx, g, (int64_t)nrb * nchunk, grid);
