@@ -8,7 +8,7 @@
 // iteration) followed by the duality gap test gap < tol * y'y.  Same operation order as
 // oracle/lasso_oracle.c (axpy = one fma per element, reductions sequential in feature order).
 //
-// One wave: lane j owns features j and j + 64 (p <= 110); H, w and q live in registers; the Gram
+// One wave (after a block-wide setup of Q): lane j owns features j and j + 64 (p <= 110); H, w and q live in registers; the Gram
 // Q sits in LDS (a row per coordinate, conflict-free); the scalar step of a coordinate is
 // computed redundantly by every lane from readlane broadcasts.  The work is a few hundred
 // flops per coordinate on a dependency chain: latency-bound by construction (one date-free
@@ -37,28 +37,32 @@ __device__ __forceinline__ double fsign(double f) { return f == 0.0 ? 0.0 : (f >
 // alpha_row >= 0: alpha = alpha_row * n (sklearn's alpha times the row count, read on the device);
 // shift / beta_out (optional): beta_out = [intercept, w] with sklearn's _set_intercept,
 // intercept = y_offset - X_offset . w over the pooled means (shift + G'[0][.] / n).
-__global__ __launch_bounds__(64) void lasso_cd_kernel(const double* gram, int p, double alpha,
+constexpr int kLassoThreads = 1024;   // the setup of Q; wave 0 alone runs the descent
+
+__global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* gram, int p, double alpha,
                                                       double beta, int max_iter, double tol,
                                                       int positive, double* w_out, double* info,
                                                       double alpha_row, const double* shift,
                                                       double* beta_out) {
     extern __shared__ double Q[];                    // [p][p] centered X'X
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int p2 = p + 2;
     const double n = gram[0];
     if (alpha_row >= 0.0) alpha = alpha_row * n;
-    // centered moments C = G'[1:,1:] - (g0 g0^T) / n of [x, y] (oracle.centered_moments)
-    for (int e = lane; e < p * p; e += 64) {
+    // centered moments C = G'[1:,1:] - (g0 g0^T) / n of [x, y] (oracle.centered_moments), by the
+    // whole block: a lone wave took ~150 dependent rounds of L2 loads and a division here
+    for (int e = tid; e < p * p; e += kLassoThreads) {
         const int i = e / p, j = e - i * p;
         Q[e] = gram[(1 + i) * p2 + 1 + j] - (gram[1 + i] * gram[1 + j]) / n;
     }
+    __syncthreads();
+    if (tid >= 64) return;
     const int j0 = lane, j1 = lane + 64;
     const bool has0 = j0 < p, has1 = j1 < p;
     double q0 = 0.0, q1 = 0.0;
     if (has0) q0 = gram[(1 + j0) * p2 + 1 + p] - (gram[1 + j0] * gram[1 + p]) / n;
     if (has1) q1 = gram[(1 + j1) * p2 + 1 + p] - (gram[1 + j1] * gram[1 + p]) / n;
     const double ynorm2 = gram[(1 + p) * p2 + 1 + p] - (gram[1 + p] * gram[1 + p]) / n;
-    __syncthreads();
 
     double h0 = 0.0, h1 = 0.0, w0 = 0.0, w1 = 0.0;  // H = Q w, w (start at 0: H = 0)
     double gap = tol + 1.0;
@@ -156,8 +160,8 @@ extern "C" int afm_lasso_cd_f64(afm_ctx* ctx, const double* gram, int p, double 
                                     (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
         attr = true;
     }
-    hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(64), lds, ctx->stream, gram, p,
-                       alpha_n, beta, max_iter, tol, positive, w, info, -1.0,
+    hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(afm::kLassoThreads), lds, ctx->stream,
+                       gram, p, alpha_n, beta, max_iter, tol, positive, w, info, -1.0,
                        (const double*)nullptr, (double*)nullptr);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
@@ -171,11 +175,15 @@ extern "C" int afm_lasso_fit_f64(afm_ctx* ctx, const double* gram, const double*
     AFM_CHECK_ARG(gram && shift && beta_out && info, "null buffer");
     AFM_CHECK_ARG(max_iter >= 1 && alpha >= 0 && tol >= 0, "bad max_iter / alpha / tol");
     const int lds = (int)sizeof(double) * p * p;
-    AFM_HIP(hipFuncSetAttribute((const void*)afm::lasso_cd_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
-    hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(64), lds, ctx->stream, gram, p, 0.0,
-                       0.0, max_iter, tol, positive, (double*)nullptr, info, alpha, shift,
+    static bool attr = false;
+    if (!attr) {
+        AFM_HIP(hipFuncSetAttribute((const void*)afm::lasso_cd_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
+        attr = true;
+    }
+    hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(afm::kLassoThreads), lds, ctx->stream,
+                       gram, p, 0.0, 0.0, max_iter, tol, positive, (double*)nullptr, info, alpha, shift,
                        beta_out);
     AFM_HIP(hipGetLastError());
     return AFM_OK;

@@ -710,27 +710,50 @@ __global__ __launch_bounds__(256) void row_bits_kernel(int64_t nch, int64_t lda,
     out[i] = w;
 }
 
-// pred[t][a] = b0 + sum_j b_j z_j, j ascending, zero coefficients skipped (wave-uniform test);
-// NaN where the row bit is clear.  One thread per cell, 4 dates x 64 assets per workgroup.
+// pred[t][a] = b0 + sum_j b_j z_j, j ascending, zero coefficients skipped; NaN where the row bit
+// is clear.  One thread per cell, 4 dates x 64 assets per workgroup.  The workgroup first
+// compacts the non-zero coefficients (ascending j, by ballot) into LDS, so a sparse Lasso costs
+// only its support per cell -- the same additions in the same order as the plain loop.
+constexpr int kPredMaxP = 128;
 __global__ __launch_bounds__(256) void zpredict_kernel(const double* base, int64_t col_stride,
                                                        int64_t lda, int64_t t0, int64_t nt,
                                                        const int32_t* cols, int p,
                                                        const double* zs, const double* beta,
                                                        const uint64_t* bits, double* pred) {
-    const int64_t a = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-    const int64_t t = t0 + (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
+    __shared__ int sj[kPredMaxP];
+    __shared__ double sb[kPredMaxP];
+    __shared__ int snnz;
+    const int tid = threadIdx.x;
+    if (tid < 64) {                                  // wave 0: j = tid, tid + 64
+        int cnt = 0;
+        for (int j0 = 0; j0 < p; j0 += 64) {
+            const int j = j0 + tid;
+            const double bj = j < p ? beta[1 + j] : 0.0;
+            const u64 m = __ballot(bj != 0.0);
+            if (bj != 0.0) {
+                const int pos = cnt + __popcll(m & ((1ull << tid) - 1ull));
+                sj[pos] = j;
+                sb[pos] = bj;
+            }
+            cnt += __popcll(m);
+        }
+        if (tid == 0) snnz = cnt;
+    }
+    __syncthreads();
+    const int nnz = snnz;
+    const int64_t a = (int64_t)blockIdx.x * 64 + (tid & 63);
+    const int64_t t = t0 + (int64_t)blockIdx.y * 4 + (tid >> 6);
     if (t >= t0 + nt) return;
     const bool use = (bits[(t >> 6) * lda + a] >> (t & 63)) & 1ull;
     double v = __builtin_nan("");
     if (use) {
         double s = beta[0];
         const double* cell = base + t * lda + a;
-        for (int j = 0; j < p; ++j) {
-            const double bj = beta[1 + j];
-            if (bj == 0.0) continue;
+        for (int q = 0; q < nnz; ++q) {
+            const int j = sj[q];
             const double2 m = reinterpret_cast<const double2*>(zs)[(int64_t)j * lda + a];
             const double z = (cell[(int64_t)cols[j] * col_stride] - m.x) * m.y;
-            s = s + bj * z;
+            s = s + sb[q] * z;
         }
         v = s;
     }
@@ -874,7 +897,7 @@ extern "C" int afm_zpredict_f64(afm_ctx* ctx, const double* base, int64_t col_st
                                 double* pred) {
     AFM_CTX(ctx);
     AFM_CHECK_ARG(base && cols && zs && beta && bits && pred, "null buffer");
-    AFM_CHECK_ARG(lda % 64 == 0 && nt >= 0 && t0 >= 0 && p >= 0, "bad shape");
+    AFM_CHECK_ARG(lda % 64 == 0 && nt >= 0 && t0 >= 0 && p >= 0 && p <= kPredMaxP, "bad shape");
     if (nt == 0) return AFM_OK;
     dim3 grid((unsigned)(lda / 64), (unsigned)((nt + 3) / 4));
     hipLaunchKernelGGL(zpredict_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride, lda, t0,
