@@ -873,46 +873,91 @@ __device__ double seq_pairwise(const double* a, int64_t n) {   // np.add.reduce,
     return seq_pairwise(a, n2) + seq_pairwise(a + n2, n - n2);
 }
 
-__global__ void xs_series_kernel(int64_t nd, const double* layer_mean, const double* port,
-                                 const double* ic, const int32_t* year, int nyears, int year0,
-                                 double* cum_layer, double* ls, double* cum_port, double* ir,
-                                 double* scratch) {
+// One workgroup.  Every series is a sequential recurrence over the dates, so each runs in one
+// lane; its inputs are read in batches of kSerB (all issued before the batch's dependent sums and
+// stores), and the per-year IC samples of the IR sit in LDS when they fit (at most 366 dates a
+// year): a lane that waited for each date's load in turn took ~0.5 ms for ~1,000 dates.
+constexpr int kSerB = 16;
+constexpr int kSerYearCap = 366;
+
+template <bool LDS_IR>
+__global__ __launch_bounds__(1024) void xs_series_kernel(int64_t nd, const double* layer_mean,
+                                                         const double* port, const double* ic,
+                                                         const int32_t* year, int nyears,
+                                                         int year0, double* cum_layer, double* ls,
+                                                         double* cum_port, double* ir,
+                                                         double* scratch) {
+    extern __shared__ double ir_lds[];                     // [3 * nyears][kSerYearCap]
     const int tid = threadIdx.x;
     if (tid < 30) {                                        // (type, layer) cumsum, NaN-skipping
         const int k = tid / 10, l = tid % 10;
         double s = 0.0;
-        for (int64_t i = 0; i < nd; ++i) {
-            const double x = layer_mean[(i * 3 + k) * kLayers + l];
-            if (x == x) {
-                s = s + x;
-                cum_layer[(i * 3 + k) * kLayers + l] = s;
-            } else {
-                cum_layer[(i * 3 + k) * kLayers + l] = qnan();
+        for (int64_t i0 = 0; i0 < nd; i0 += kSerB) {
+            double xb[kSerB];
+#pragma unroll
+            for (int j = 0; j < kSerB; ++j)
+                xb[j] = i0 + j < nd ? layer_mean[((i0 + j) * 3 + k) * kLayers + l] : 0.0;
+#pragma unroll
+            for (int j = 0; j < kSerB; ++j) {
+                if (i0 + j >= nd) break;
+                const double x = xb[j];
+                double* o = &cum_layer[((i0 + j) * 3 + k) * kLayers + l];
+                if (x == x) {
+                    s = s + x;
+                    *o = s;
+                } else {
+                    *o = qnan();
+                }
             }
         }
     } else if (tid < 33) {
         const int k = tid - 30;
         double s = 0.0;
-        for (int64_t i = 0; i < nd; ++i) {
-            s = s + port[i * 3 + k];
-            cum_port[i * 3 + k] = s;
+        for (int64_t i0 = 0; i0 < nd; i0 += kSerB) {
+            double xb[kSerB];
+#pragma unroll
+            for (int j = 0; j < kSerB; ++j) xb[j] = i0 + j < nd ? port[(i0 + j) * 3 + k] : 0.0;
+#pragma unroll
+            for (int j = 0; j < kSerB; ++j) {
+                if (i0 + j >= nd) break;
+                s = s + xb[j];
+                cum_port[(i0 + j) * 3 + k] = s;
+            }
         }
     }
     __syncthreads();
     if (tid < 15) {                                        // long-short: cum[10-l+1] - cum[l]
         const int k = tid / 5, l = tid % 5 + 1;
-        for (int64_t i = 0; i < nd; ++i)
-            ls[(i * 3 + k) * 5 + (l - 1)] =
-                cum_layer[(i * 3 + k) * kLayers + (kLayers - l)] - cum_layer[(i * 3 + k) * kLayers + (l - 1)];
+        for (int64_t i0 = 0; i0 < nd; i0 += kSerB) {
+            double hb[kSerB], lb[kSerB];
+#pragma unroll
+            for (int j = 0; j < kSerB; ++j) {
+                const int64_t i = i0 + j < nd ? i0 + j : nd - 1;
+                hb[j] = cum_layer[(i * 3 + k) * kLayers + (kLayers - l)];
+                lb[j] = cum_layer[(i * 3 + k) * kLayers + (l - 1)];
+            }
+#pragma unroll
+            for (int j = 0; j < kSerB; ++j)
+                if (i0 + j < nd) ls[((i0 + j) * 3 + k) * 5 + (l - 1)] = hb[j] - lb[j];
+        }
     }
     if (tid >= 64 && tid < 64 + 3 * nyears) {              // IR per (year, type)
         const int q = tid - 64;
         const int y = q / 3, k = q % 3;
-        double* buf = scratch + (int64_t)q * nd;
+        double* buf = LDS_IR ? ir_lds + (int64_t)q * kSerYearCap : scratch + (int64_t)q * nd;
         int64_t n = 0;
-        for (int64_t i = 0; i < nd; ++i) {
-            const double x = ic[i * 3 + k];
-            if (year[i] == year0 + y && x == x) buf[n++] = x;
+        for (int64_t i0 = 0; i0 < nd; i0 += kSerB) {
+            double xb[kSerB];
+            int yb[kSerB];
+#pragma unroll
+            for (int j = 0; j < kSerB; ++j) {
+                const int64_t i = i0 + j < nd ? i0 + j : nd - 1;
+                xb[j] = ic[i * 3 + k];
+                yb[j] = year[i];
+            }
+#pragma unroll
+            for (int j = 0; j < kSerB; ++j)
+                if (i0 + j < nd && yb[j] == year0 + y && xb[j] == xb[j]) buf[n++] = xb[j];
         }
         double res = qnan();
         if (n > 0) {
@@ -1141,8 +1186,23 @@ extern "C" int afm_xs_series_f64(afm_ctx* ctx, int64_t nd, const double* layer_m
     AFM_CHECK_ARG(layer_mean && port && ic && year && cum_layer && ls && cum_port && ir &&
                       scratch, "null buffer");
     if (nd <= 0) return AFM_OK;
-    hipLaunchKernelGGL(xs_series_kernel, dim3(1), dim3(1024), 0, ctx->stream, nd, layer_mean,
-                       port, ic, year, nyears, year0, cum_layer, ls, cum_port, ir, scratch);
+    // the per-year IC samples in LDS when they fit (at most kSerYearCap dates a year)
+    const size_t lds = sizeof(double) * (size_t)(3 * nyears) * kSerYearCap;
+    if (lds <= 150 * 1024) {
+        static bool attr = false;
+        if (!attr) {
+            AFM_HIP(hipFuncSetAttribute((const void*)xs_series_kernel<true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+            attr = true;
+        }
+        hipLaunchKernelGGL(xs_series_kernel<true>, dim3(1), dim3(1024), lds, ctx->stream, nd,
+                           layer_mean, port, ic, year, nyears, year0, cum_layer, ls, cum_port, ir,
+                           scratch);
+    } else {
+        hipLaunchKernelGGL(xs_series_kernel<false>, dim3(1), dim3(1024), 0, ctx->stream, nd,
+                           layer_mean, port, ic, year, nyears, year0, cum_layer, ls, cum_port, ir,
+                           scratch);
+    }
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }
