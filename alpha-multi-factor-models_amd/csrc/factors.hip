@@ -769,9 +769,8 @@ struct Pack<H, R...> {
     __device__ void init() { h.init(); r.init(); }
     __device__ void step(Step& s) { h.step(s); r.step(s); }
     __device__ void fstep(Step& s) {
-        h.fstep(s);
-        __builtin_amdgcn_sched_barrier(0);      // jobs one after another: bounds VGPR pressure
-        r.fstep(s);
+        h.fstep(s);     // no scheduling barrier: the compiler interleaves the jobs' independent
+        r.fstep(s);     // chains (12.55 -> 12.32 ms at config C, bit-identical)
     }
 };
 
