@@ -458,17 +458,25 @@ class Pipeline:
             mark("xs_gram", 1)
             # side stream: this shard's per-date FM30 partials (nothing downstream reads them),
             # forked after the pooled Gram -- run beside it, both MFMA kernels slow down (A/B on
-            # MI355X: pooled Gram 12.7 ms alone, 23 ms beside the FM Grams)
-            self.side.wait_stream(self.main)
-            with torch.cuda.stream(self.side):
-                hs = self.ctx.bind_stream()
-                mark("fm", 0)
-                self._fm_local(hs)
-                if W == 1:
-                    self._fm_solve(hs, self.fm_sub)
-                    self._fm_stats(hs)
-                mark("fm", 1)
-            h = self.ctx.bind_stream()
+            # MI355X: pooled Gram 12.7 ms alone, 23 ms beside the FM Grams).  One GPU: forked
+            # after the predict, ahead of the analyzer (A/B over 5 runs: 35.29 vs 35.40 ms/step
+            # forked after the Gram; 36.4-37.0 after the analyzer, 36.5-36.7 after the
+            # rebalance).  AFM_FM_FORK=gram|predict|analyzer|rebalance: A/B.
+            def fork_fm():
+                self.side.wait_stream(self.main)
+                with torch.cuda.stream(self.side):
+                    hs = self.ctx.bind_stream()
+                    mark("fm", 0)
+                    self._fm_local(hs)
+                    if W == 1:
+                        self._fm_solve(hs, self.fm_sub)
+                        self._fm_stats(hs)
+                    mark("fm", 1)
+                return self.ctx.bind_stream()
+
+            fm_at = os.environ.get("AFM_FM_FORK", "predict") if W == 1 else "gram"
+            if fm_at == "gram":
+                h = fork_fm()
             mark("lasso", 0)
             chk(L.afm_lasso_fit_f64(h, P(self.pool_g), P(self.pool_s), p, c.alpha, c.max_iter,
                                     c.lasso_tol, 0, P(self.lasso_beta), P(self.lasso_info)),
@@ -483,11 +491,15 @@ class Pipeline:
                 self._gather_test_planes()
                 h = self.ctx.bind_stream()
             mark("predict", 1)
+            if fm_at == "predict":
+                h = fork_fm()
             if c.analyzer:
                 self.side2.wait_stream(self.main)
                 with torch.cuda.stream(self.side2):
                     self._analyzer(mark)
                 h = self.ctx.bind_stream()
+            if fm_at == "analyzer":
+                h = fork_fm()
             mark("rebalance", 0)
             if W > 1:
                 self.main.wait_event(self.labels_done)     # the label planes
@@ -504,6 +516,8 @@ class Pipeline:
                 self._gather_rebalance()
                 h = self.ctx.bind_stream()
             mark("rebalance", 1)
+            if fm_at == "rebalance":
+                h = fork_fm()
             mark("pnl", 0)
             r, q = self.reb, self.pnl
             chk(L.afm_pnl_scan_f64(h, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]),
