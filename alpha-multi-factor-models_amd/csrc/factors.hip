@@ -778,22 +778,25 @@ struct Pack<H, R...> {
 // the compiled step: Corr ~550, RetSd5x15 ~360, VolSd5x15 ~290, BB ~220, VWMA ~170, RetSd3 /
 // VolSd3 / PvtObvPsy ~155, RSI ~115, SMA / MomAccelRocr ~100, MACD ~75, EMA ~60; ~620 per wave),
 // then waves placed so the four SIMDs (waves w, w+4, w+8, w+12; the loader shares SIMD 3) carry
-// equal totals.
+// equal totals.  Round 2: SMA_6 moved from W1 to W13 and EMA_6 from W8 to W14 so the three 3-way
+// item types take equal time (per-type max 25.0 / 25.0 / 22.2 -> 25.1 / 25.1 / 24.1 Mcycles,
+// 12.28 -> 11.46 ms at config C, no spill in the fast steps; a move that made the fast steps
+// spill measured 14.7 ms).
 using W0 = Pack<Bbands<14>, Vwma<30>, MomAccelRocr<32>, Sma<42>, Ema<50>>;
-using W1 = Pack<Bbands<44>, Vwma<50>, Sma<6>, Sma<38>, Ema<46>>;
+using W1 = Pack<Bbands<44>, Vwma<50>, Sma<38>, Ema<46>>;
 using W2 = Pack<Bbands<50>, RetSd3, MomAccelRocr<26>, Sma<34>, Ema<42>>;
 using W3 = Pack<Bbands<56>, VolSd3, MomAccelRocr<20>, Sma<30>, Ema<38>>;
 using W4 = Pack<Vwma<6>, Vwma<18>, Rsi<8>, Sma<18>, Ema<18>>;
 using W5 = Pack<RetSd5x15, MomAccelRocr<14>, Sma<14>, Ema<14>>;
 using W6 = Pack<Bbands<38>, Vwma<46>, MomAccelRocr<56>, Macd<24>, Ema<34>>;
 using W7 = Pack<Bbands<32>, Vwma<42>, MomAccelRocr<50>, Macd<18>, Ema<30>>;
-using W8 = Pack<VolSd5x15, PvtObvPsy, Sma<10>, Ema<6>>;
+using W8 = Pack<VolSd5x15, PvtObvPsy, Sma<10>>;
 using W9 = Pack<Corr<5, true>, Ema<10>>;
 using W10 = Pack<Vwma<14>, Vwma<26>, Rsi<20>, Sma<26>, Ema<26>>;
 using W11 = Pack<Vwma<10>, Vwma<22>, Rsi<14>, Sma<22>, Ema<22>>;
 using W12 = Pack<Corr<15, false>, Macd<30>>;
-using W13 = Pack<Bbands<20>, Vwma<34>, MomAccelRocr<38>, Sma<46>>;
-using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>>;
+using W13 = Pack<Bbands<20>, Vwma<34>, MomAccelRocr<38>, Sma<46>, Sma<6>>;
+using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>, Ema<6>>;
 
 // The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
 // job waves (one per chunk + two at each 64-day word end).  It also publishes, per lane and
@@ -1063,8 +1066,9 @@ constexpr int kStateWords = cmax(cmax(cmax(cmax(state_words<W0>(), state_words<W
 // second round; paired, 236 workgroups of 12 waves (3 per SIMD, 156 KB LDS) are all resident.
 // Paired 3-way launch: job (0-4) or loader (5) run at wave position k of each half, per type.
 // Wave w of a workgroup issues on SIMD w % 4; the layouts minimise the busiest SIMD's measured
-// cycles (tools/wave_profile.py; type 1: 61.3 -> 55.0 Mcycles).
-__constant__ const signed char kPairLayout[3][2][6] = {
+// cycles (tools/wave_profile.py; type 1: 61.3 -> 55.0 Mcycles; round 2 re-checked for the new
+// partition with AFM_FP_LAYOUT, tools/gpu_layout.sh: four other layouts per type, none faster).
+__constant__ signed char kPairLayout[3][2][6] = {
     {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
     {{0, 2, 3, 4, 1, 5}, {1, 2, 3, 4, 0, 5}},
     {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
@@ -1273,6 +1277,17 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     if (const char* e = getenv("AFM_FP_NOFAST"))                   // A/B: general step only
         a.fast = atoi(e) ? 0 : 1;
     const dim3 grid((unsigned)(nblk * types));
+    static bool layout_set = false;                   // tuning override of kPairLayout:
+    if (!layout_set) {                                // 36 digits, [type][half][position]
+        layout_set = true;
+        if (const char* e = getenv("AFM_FP_LAYOUT")) {
+            signed char l[36];
+            int n = 0;
+            for (; e[n] && n < 36; ++n) l[n] = (signed char)(e[n] - '0');
+            if (n == 36)
+                AFM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(afm::kPairLayout), l, sizeof(l)));
+        }
+    }
     static bool lds_attr = false;                     // > 64 KB of dynamic LDS: opt in once
     if (!lds_attr) {
         const int bytes = (int)sizeof(afm::Smem);

@@ -8,7 +8,7 @@ if [ -n "$LAT" ] && [ -x tools/lat_probe/lat_probe ]; then
 fi
 for v in default ${FP_VARIANTS}; do
   if [ $v = default ]; then L=""; else L=$GRAFT_REPO_ROOT/alpha-multi-factor-models_amd/build/zgv/$v/libafm.so; fi
-  AFM_LIB=$L timeout -k 10 240 python -u tools/fp_probe.py > gpurun_out/fpab_$v.log 2>&1 || { tail -20 gpurun_out/fpab_$v.log; exit 1; }
+  AFM_LIB=$L timeout -k 10 240 python -u tools/fp_probe.py --reps ${FP_REPS:-5} > gpurun_out/fpab_$v.log 2>&1 || { tail -20 gpurun_out/fpab_$v.log; exit 1; }
   grep factors gpurun_out/fpab_$v.log
   if [ -n "$FP_TEST" ]; then
     AFM_LIB=$L timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_factors_gpu.py > gpurun_out/fpab_test_$v.log 2>&1 || { tail -20 gpurun_out/fpab_test_$v.log; exit 1; }
