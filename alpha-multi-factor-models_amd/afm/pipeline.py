@@ -475,6 +475,9 @@ class Pipeline:
                 return self.ctx.bind_stream()
 
             fm_at = os.environ.get("AFM_FM_FORK", "predict") if W == 1 else "gram"
+            if fm_at not in ("gram", "predict", "analyzer", "rebalance"):
+                raise ValueError(f"AFM_FM_FORK={fm_at!r}: expected gram, predict, analyzer or "
+                                 "rebalance")
             if fm_at == "gram":
                 h = fork_fm()
             mark("lasso", 0)
