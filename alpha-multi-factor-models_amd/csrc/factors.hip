@@ -1284,8 +1284,17 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
             signed char l[36];
             int n = 0;
             for (; e[n] && n < 36; ++n) l[n] = (signed char)(e[n] - '0');
-            if (n == 36)
-                AFM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(afm::kPairLayout), l, sizeof(l)));
+            bool ok = n == 36 && e[n] == 0;
+            for (int h = 0; ok && h < 6; ++h) {           // each (type, half): a permutation of 0..5
+                int seen = 0;
+                for (int q = 0; q < 6; ++q) {
+                    const int v = l[6 * h + q];
+                    if (v < 0 || v > 5 || (seen >> v) & 1) ok = false;
+                    else seen |= 1 << v;
+                }
+            }
+            AFM_CHECK_ARG(ok, "AFM_FP_LAYOUT: 36 digits, each group of 6 a permutation of 0..5");
+            AFM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(afm::kPairLayout), l, sizeof(l)));
         }
     }
     static bool lds_attr = false;                     // > 64 KB of dynamic LDS: opt in once
