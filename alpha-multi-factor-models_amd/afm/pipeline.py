@@ -407,10 +407,22 @@ class Pipeline:
         with torch.cuda.stream(self.main):
             h = self.ctx.bind_stream()
             mark("factors", 0)
+            # one GPU: the two label planes on the side stream, enqueued after the factor kernel
+            # (it runs on the CUs the factor workgroups leave free); zstats waits for them
+            lab_side = W == 1 and os.environ.get("AFM_LABELS_SIDE", "1") != "0"
             if self.A_r > 0:
                 chk(L.afm_factors_f64(h, T, self.A_r, lda_r, P(g.close), P(g.volume),
-                                      P(g.ret1d), P(g.excess), P(g.vbits), P(self.out),
+                                      None if lab_side else P(g.ret1d),
+                                      None if lab_side else P(g.excess), P(g.vbits), P(self.out),
                                       P(self.nanfree), P(self.finite)), "factors")
+                if lab_side:
+                    with torch.cuda.stream(self.side2):
+                        h2 = self.ctx.bind_stream()
+                        chk(L.afm_labels_f64(h2, T, lda_r, 0, T, P(g.excess), P(g.ret1d),
+                                             P(g.vbits), P(self.out[TARGET]), P(self.out[TMR])),
+                            "labels")
+                        self.labels_done.record(self.side2)
+                    h = self.ctx.bind_stream()
                 chk(L.afm_drop_last_obs_bits(h, T, lda_r, P(g.vbits), P(self.nanfree),
                                              P(self.alldf)), "all_df rows")
                 chk(L.afm_drop_last_obs_bits(h, T, lda_r, P(g.vbits), P(self.finite),
@@ -418,6 +430,8 @@ class Pipeline:
             mark("factors", 1)
             mark("zstats", 0)
             if self.A_r > 0:
+                if lab_side:
+                    self.main.wait_event(self.labels_done)          # tmr_ret1d is a feature
                 chk(L.afm_zscore_stats_f64(h, P(self.out), T * lda_r, T, lda_r, P(self.feat), p,
                                            P(self.alldf), 0, sp.tr1, P(self.mu), P(self.sd)),
                     "zscore stats")

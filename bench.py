@@ -31,6 +31,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md chip table)
 F64_MFMA_PEAK_TFS = 78.6       # MI355X fp64 matrix peak (spec)
 FACTOR_BYTES_PER_AD = 816      # 4 x 8 B inputs read + 98 x 8 B outputs written
+# the factor stage without the two label planes (they run on a side stream beside the factor
+# kernel: afm/pipeline.py): close + volume read, 96 columns written
+FACTOR_BYTES_NO_LABELS = 784
 
 
 def log(*a):
@@ -41,6 +44,7 @@ def log(*a):
 # FETCH_SIZE x2 and KiB corrections of MI355X_MICROARCH.md applied there)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
 ROOF_KERNELS = {"factors": ("factor_panel_kernel", "masks_kernel", "labels_kernel"),
+                "factors_nolabels": ("factor_panel_kernel", "masks_kernel"),
                 "xs_gram": ("zgram_kernel<7, 1, true>",)}
 
 
@@ -193,9 +197,12 @@ def main():
         ms = elapsed / args.steps * 1e3
         p2 = pipe.p2
         # roofline of the two dominant kernels, ranked by per-step device time: the factor panel
-        # (HBM: 816 B per asset-day) and the pooled Gram (fp64 MFMA:
+        # (HBM: 816 B per asset-day; 784 B without the two label planes, which
+        # run on a side stream beside the factor kernel) and the pooled Gram (fp64 MFMA:
         # rows * (p+2)(p+3) flops over the train + valid rows, zpool + tree merges).
-        fac_gbs = FACTOR_BYTES_PER_AD * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
+        labels_in = world == 1 and os.environ.get("AFM_LABELS_SIDE", "1") == "0"
+        fac_bytes = FACTOR_BYTES_PER_AD if labels_in else FACTOR_BYTES_NO_LABELS
+        fac_gbs = fac_bytes * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
         rows_tv = float(pipe.pool_g[0, 0, 0].item())           # pooled rows (n of the Gram)
         if pipe.sp.dup:
             rows_tv -= float(pipe.te_gram[0, 0, 0].item())       # the duplicate is not recomputed
@@ -204,10 +211,13 @@ def main():
         single = world == 1
         fac = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(fac_gbs / HBM_PEAK_GBS, 4),
-               "traffic": None, "kernel": "factor_panel_kernel (+ row-bit kernels)",
+               "traffic": None,
+               "kernel": "factor_panel_kernel (+ masks, row-bit kernels%s)" % (
+                   ", label planes" if labels_in else "; label planes on a side stream"),
                "kernel_ms": round(stage_ms["factors"], 3),
-               "algorithmic_GB": round(FACTOR_BYTES_PER_AD * n_ad_local / 1e9, 3)}
-        tb = pmc_traffic("factors", args.assets, args.days) if single else None
+               "algorithmic_GB": round(fac_bytes * n_ad_local / 1e9, 3)}
+        tb = (pmc_traffic("factors" if labels_in else "factors_nolabels", args.assets, args.days)
+              if single else None)
         if tb is not None:
             fac["traffic"] = round(tb / 1e9, 3)
             fac["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
