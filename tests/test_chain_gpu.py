@@ -127,3 +127,24 @@ def test_fama_macbeth_vs_golden(chain_a):
     assert (rk[d[ok]] == pf).all()
     err = np.abs(fb[d[ok]] - B[ok]).max(axis=1) / np.abs(B[ok]).max(axis=1)
     assert err.max() < 1e-9, err.max()
+
+
+@pytest.mark.parametrize("env", [("AFM_LABELS_SIDE", "0"), ("AFM_FM_FORK", "gram"),
+                                 ("AFM_FM_FORK", "rebalance")])
+def test_stream_placement_bit_identical(chain_a, env, monkeypatch):
+    """The side-stream placements (label planes beside the factor kernel, the FM fork point) move
+    work between streams only: the step's outputs are bitwise those of the default placement."""
+    import torch
+    from afm.pipeline import Pipeline, PipelineConfig
+    p, pipe, gold, C = chain_a
+    monkeypatch.setenv(*env)
+    other = Pipeline(pipe.g, PipelineConfig(train_end=C["train_end"], valid_end=C["valid_end"],
+                                            window=C["window"], top_n=C["top_n"]))
+    other.step()
+    torch.cuda.synchronize()
+    for name in ("out", "pred", "lasso_beta", "fm_beta"):
+        a, b = getattr(pipe, name), getattr(other, name)
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64)), name
+    for k in ("k", "books", "weights"):
+        assert torch.equal(pipe.reb[k], other.reb[k]), k
+    assert torch.equal(pipe.pnl["value"], other.pnl["value"])
