@@ -23,6 +23,7 @@ DBL = ctypes.c_double
 SIGNATURES = {
     "afm_ctx_create": (I32, [I32, ctypes.POINTER(P)]),
     "afm_ctx_set_stream": (I32, [P, P]),
+    "afm_ctx_set_option": (I32, [P, ctypes.c_char_p, I64]),
     "afm_ctx_destroy": (I32, [P]),
     "afm_last_error": (ctypes.c_char_p, []),
     "afm_version": (I32, []),
@@ -129,6 +130,11 @@ class Context:
             ctx = cls._by_device[device] = Context(device)
         return ctx
 
+    def set_option(self, name: str, value: int):
+        """afm_ctx_set_option: an execution option of this context (include/afm.h)."""
+        check(lib().afm_ctx_set_option(self.handle, name.encode(), int(value)),
+              f"afm_ctx_set_option({name})")
+
     def bind_stream(self):
         import torch
         s = torch.cuda.current_stream(self.device).cuda_stream
@@ -146,3 +152,24 @@ def ptr(t) -> P:
 def factor_names() -> list:
     L = lib()
     return [L.afm_factor_name(i).decode() for i in range(98)]
+
+
+class options:
+    """Context manager: execution options of the device's context (afm_ctx_set_option) for the
+    duration of a block, restored to the defaults after -- the invariance tests' work splits."""
+
+    DEFAULTS = {"factor_split": 0, "factor_pair": 1, "factor_fast": 1, "gram_checked": 0}
+
+    def __init__(self, device: int | None = None, **opts):
+        self.device, self.opts = device, opts
+
+    def __enter__(self):
+        self.ctx = Context.get(self.device)
+        for k, v in self.opts.items():
+            self.ctx.set_option(k, v)
+        return self.ctx
+
+    def __exit__(self, *exc):
+        for k in self.opts:
+            self.ctx.set_option(k, self.DEFAULTS[k])
+        return False

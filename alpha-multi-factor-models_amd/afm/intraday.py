@@ -149,7 +149,8 @@ def factor_panel_groups(grid: PanelGrid, consumer, blocks_per_group: int | None 
 def slab_bars(grid: PanelGrid, budget_bytes: int | None = None) -> int:
     """Bars per time slab: the most (a multiple of 64) whose output planes and mask words fit in
     ``budget_bytes`` (default: 85% of the free HBM), balanced so the slabs have near-equal
-    lengths."""
+    lengths.  Always a multiple of 64 (slab starts must be word-aligned); it may exceed T when
+    one slab holds the whole series -- factor_panel_slabs clamps the last slab to T."""
     import torch
     T, lda = grid.T, grid.lda
     if budget_bytes is None:
@@ -158,7 +159,7 @@ def slab_bars(grid: PanelGrid, budget_bytes: int | None = None) -> int:
     per_bar = N_FACTORS * 8 * lda + 2 * 8 * lda // 64 + 16
     cap = max(64, (budget_bytes // per_bar) // 64 * 64)
     n = (T + cap - 1) // cap
-    return min(T, ((T + n - 1) // n + 63) // 64 * 64)
+    return ((T + n - 1) // n + 63) // 64 * 64
 
 
 def factor_panel_slabs(grid: PanelGrid, consumer, bars_per_slab: int | None = None):

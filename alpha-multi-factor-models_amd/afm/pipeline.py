@@ -63,6 +63,10 @@ FM30 = ["tmr_ret1d", "ACCEL_32", "sd5_15", "corr_5", "OBV", "sd_15", "MOM_38", "
         "vol_change", "volsd_15", "corr_15", "ACCEL_38", "BBANDS_upper_14", "ACCEL_20",
         "ACCEL_26", "ROCR_14", "sd_3", "ACCEL_50", "volsd_3", "ACCEL_44", "ACCEL_56", "ROCR_20",
         "ROCR_56", "PVT", "PSY", "ROCR_32", "MOM_26", "ACCEL_14", "RSI_8", "MOM_50"]
+# a non-reference variant of KKT:433-443 (bench.py's "dense_lasso" line): the 96 factors without
+# tmr_ret1d.  With tmr_ret1d in the design the Lasso keeps one coefficient (the headline step
+# reads one plane in the predict); without it the fit is dense.
+DENSE_FEATURES = tuple(n for n in FEATURES if n != "tmr_ret1d")
 N_BLOCKS = 8           # fixed asset blocks of the Gram trees (>= the largest GPU count)
 N_CHUNKS = 64          # date chunks of the pooled Gram's row-block partials (2 tree levels)
 CHUNK_TREE = (32, 2)   # the chunks of a row-block: groups of 32, then the 2 results
@@ -89,6 +93,10 @@ class PipelineConfig:
     v0: float = 100000000.0         # KKT:804
     tol: float = 1e-10              # pivot threshold of the per-date solve
     analyzer: bool = True
+    # the regression design: None = the reference's 97 columns (KKT:433-443, FEATURES).  A stated
+    # variant may name another subset -- e.g. DENSE_FEATURES, which drops tmr_ret1d (the
+    # undemeaned twin of the target, NT:90-91) so the Lasso keeps many coefficients
+    features: tuple | None = None
 
 
 @dataclass
@@ -155,7 +163,8 @@ class Pipeline:
         nch = (T + 63) // 64
         self.T, self.lda, self.A, self.nch = T, lda, A, nch
         self.sp = sp = Split.of(grid.dates, c.train_end, c.valid_end)
-        self.p = p = len(FEATURES)
+        self.features = list(c.features) if c.features is not None else FEATURES
+        self.p = p = len(self.features)
         self.p2 = p + 2
         self.pf = len(c.fm_features)
         f64 = dict(dtype=torch.float64, device=dev)
@@ -168,6 +177,10 @@ class Pipeline:
         self.nblk = N_BLOCKS
         self.blk = blk = block_assets(lda)
         self.rb_per_blk = blk // 64
+        if self.rb_per_blk > 32:          # afm_gram_tree_f64 merges at most 32 leaves a level
+            raise ValueError(f"{A} assets: the pooled-Gram tree holds at most "
+                             f"{N_BLOCKS * 32 * 64} assets ({N_BLOCKS} blocks x 32 row-blocks "
+                             f"of 64)")
         self.nblk_r = N_BLOCKS // W
         self.ranges = []
         for q in range(W):
@@ -188,7 +201,8 @@ class Pipeline:
                                excess=grid.excess[:, sl].contiguous(),
                                valid=grid.valid[:, sl].contiguous(),
                                vbits=grid.vbits[:, sl].contiguous())
-        self.feat = torch.as_tensor(np.array([COL[n] for n in FEATURES], np.int32), device=dev)
+        self.feat = torch.as_tensor(np.array([COL[n] for n in self.features], np.int32),
+                                    device=dev)
         # ---- local (shard) buffers ----
         self.out = torch.full((N_FACTORS, T, lda_r), float("nan"), **f64)
         self.nanfree = torch.zeros((nch, lda_r), **i64)

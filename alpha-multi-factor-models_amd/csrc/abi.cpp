@@ -1,9 +1,25 @@
 // Context, error and metadata entry points of the C-ABI (include/afm.h).
 #include "afm_internal.h"
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 static thread_local std::string g_last_error;
 
 void afm_set_error(const std::string& msg) { g_last_error = msg; }
+
+hipError_t afm_lds_opt_in(const afm_ctx* ctx, const void* kernel, int bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, int> done;    // (kernel, device) -> bytes set
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair(kernel, ctx->device);
+    auto it = done.find(key);
+    if (it != done.end() && it->second >= bytes) return hipSuccess;
+    hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done[key] = bytes;
+    return e;
+}
 
 extern "C" {
 
@@ -26,6 +42,26 @@ int afm_ctx_create(int device, afm_ctx** out) {
 int afm_ctx_set_stream(afm_ctx* ctx, void* stream) {
     AFM_CTX(ctx);
     ctx->stream = reinterpret_cast<hipStream_t>(stream);
+    return AFM_OK;
+}
+
+int afm_ctx_set_option(afm_ctx* ctx, const char* name, int64_t value) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(name != nullptr, "name is null");
+    const std::string n(name);
+    if (n == "factor_split") {
+        AFM_CHECK_ARG(value == 0 || value == 1 || value == 3 || value == 5 || value == 15,
+                      "factor_split: 0 (auto), 1, 3, 5 or 15");
+        ctx->factor_split = (int)value;
+    } else if (n == "factor_pair") {
+        ctx->factor_pair = value != 0;
+    } else if (n == "factor_fast") {
+        ctx->factor_fast = value != 0;
+    } else if (n == "gram_checked") {
+        ctx->gram_checked = value != 0;
+    } else {
+        AFM_CHECK_ARG(false, "unknown option " + n);
+    }
     return AFM_OK;
 }
 

@@ -12,9 +12,20 @@ struct afm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int magic = 0x61666d31;  // "afm1"
+    // execution options (afm_ctx_set_option): work splits that must not change any result, set
+    // by the invariance tests; 0 = the library's choice
+    int factor_split = 0;    // workgroups per 64-asset block of the factor kernel (1, 3, 5, 15)
+    int factor_pair = 1;     // 3-way split: two items per workgroup
+    int factor_fast = 1;     // clean-window fast step on
+    int gram_checked = 0;    // afm_xs_gram_f64: checked staging only (no FAST + REDO passes)
 };
 
 void afm_set_error(const std::string& msg);
+
+// Opt a kernel in to `bytes` of dynamic LDS on the context's device (> 64 KB needs it).  The
+// attribute is per device, so the memo is keyed by (kernel, device): a process that drives
+// several GPUs sets it on each.
+hipError_t afm_lds_opt_in(const afm_ctx* ctx, const void* kernel, int bytes);
 
 #define AFM_CHECK_ARG(cond, msg)                                   \
     do {                                                           \

@@ -1092,7 +1092,11 @@ extern "C" int afm_xs_prepare_range_f64(afm_ctx* ctx, int64_t T, int64_t A, int6
     AFM_CHECK_ARG(sig && fr && scratch && rows && rows_idx && nrows, "null buffer");
     if (t1 == t0) return AFM_OK;
     PrepArgs g{T, lda, A, sig, fr, scratch, rows, rows_idx, nrows, t0, nullptr, nullptr};
+#ifdef AFM_PROBE                     // profiling build (make prof): phase timestamps
     const bool probe = getenv("AFM_AN_PROBE") != nullptr;
+#else
+    const bool probe = false;
+#endif
     if (probe) AFM_HIP(hipMalloc((void**)&g.stamps, sizeof(int64_t) * T * 5));
     if (probe) AFM_HIP(hipMalloc((void**)&g.clk, sizeof(int64_t) * T * 2));
     hipLaunchKernelGGL(xs_prepare_kernel, dim3((unsigned)(t1 - t0)), dim3(kPT), 0, ctx->stream, g);
@@ -1134,12 +1138,7 @@ extern "C" int afm_xs_rank_f64(afm_ctx* ctx, int64_t T, int64_t lda, const doubl
     const size_t sort_bytes = (sizeof(u64) + sizeof(int32_t)) * kChunk;
     int lds_rows = (int)(lda < 12288 ? lda : 12288);
     const size_t lds = std::max(sort_bytes, (size_t)lds_rows * 12);
-    static bool attr = false;
-    if (!attr) {
-        AFM_HIP(hipFuncSetAttribute((const void*)xs_rank_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 12288 * 12));
-        attr = true;
-    }
+    AFM_HIP(afm_lds_opt_in(ctx, (const void*)xs_rank_kernel, 12288 * 12));
     hipLaunchKernelGGL(xs_rank_kernel, dim3((unsigned)T), dim3(kWT), lds, ctx->stream, g,
                        lds_rows);
     AFM_HIP(hipGetLastError());
@@ -1189,12 +1188,7 @@ extern "C" int afm_xs_series_f64(afm_ctx* ctx, int64_t nd, const double* layer_m
     // the per-year IC samples in LDS when they fit (at most kSerYearCap dates a year)
     const size_t lds = sizeof(double) * (size_t)(3 * nyears) * kSerYearCap;
     if (lds <= 150 * 1024) {
-        static bool attr = false;
-        if (!attr) {
-            AFM_HIP(hipFuncSetAttribute((const void*)xs_series_kernel<true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
-            attr = true;
-        }
+        AFM_HIP(afm_lds_opt_in(ctx, (const void*)xs_series_kernel<true>, 150 * 1024));
         hipLaunchKernelGGL(xs_series_kernel<true>, dim3(1), dim3(1024), lds, ctx->stream, nd,
                            layer_mean, port, ic, year, nyears, year0, cum_layer, ls, cum_port, ir,
                            scratch);

@@ -10,7 +10,8 @@
 //    per asset.  Parallelism = assets (one per lane) x indicator jobs (one job set per wave).
 //  * One workgroup = one 64-asset block: 15 job waves (balanced by the VALU count of each job's
 //    compiled step, and so that the four SIMDs carry equal totals) + 1 loader wave; the kernel
-//    is VALU-issue-bound (~86% of each SIMD's cycles).  An LDS ring holds the last kRing
+//    is bound by f64 dependency latency at ~2.3 job waves per SIMD (~50 % VALU-busy, DESIGN.md
+//    §4).  An LDS ring holds the last kRing
 //    present observations of close and volume per lane.  A shard with few blocks (multi-GPU)
 //    splits each block's 15 job waves over 3, 5 or 15 workgroups instead, so that ~all CUs work
 //    (each split needs its own ring; measured on MI355X, workgroups of 78 KB LDS do not
@@ -47,14 +48,7 @@ constexpr int kLanes = 64;
 constexpr int kChunk = 8;
 // the loader fills chunk c+1 while the job waves scan chunk c: the ring must hold the scan's
 // lookback (57) plus two chunks
-#ifdef AFM_FP_RING
-constexpr int kRing = AFM_FP_RING;     // experiments only
-#else
 constexpr int kRing = 57 + 2 * kChunk + 1;
-#endif
-#ifndef AFM_FP_WPE3
-#define AFM_FP_WPE3 3
-#endif
 constexpr int kJobSets = 15;      // job waves per 64-asset block (W0..W14 below)
 
 typedef unsigned long long u64;
@@ -82,7 +76,7 @@ struct Smem {
     double v[kRing][kLanes];   // volume ring
     double rtab[128];          // rtab[n] = 1.0 / n (IEEE), rtab[0] = +inf; indexed n & 127
     int cbyte[2][kLanes];      // presence bits of chunk c (parity c & 1), written by the loader
-    int okbyte[2][kLanes];     // 1 = every present day of chunk c has a clean window (see kClean)
+    int okbyte[2][kLanes];     // chunk c: 2 every present day clean (kClean), 1 warm, 0 general
     u64 nanmask[kLanes];
     u64 badmask[kLanes];       // some factor non-finite (NaN or +-inf)
 };
@@ -278,6 +272,13 @@ struct RollMean {
     __device__ __forceinline__ void fsigns(double xadd, double xrem) {
         neg += (__builtin_signbit(xadd) ? 1 : 0) - (__builtin_signbit(xrem) ? 1 : 0);
     }
+    // warm window (see "warm-up windows" below): the Kahan cores, remove value 0 before the window
+    // is full (exactly a no-op while crem is still +0), the count kept for the general step
+    __device__ __forceinline__ void wstep(double xrem, double xadd, int n) {
+        fremove(xrem);
+        fadd(xadd);
+        nobs = n;
+    }
     template <int W>
     __device__ __forceinline__ double fresult(const Run& rn) const {
         double r = divc<W>(sum);
@@ -343,6 +344,14 @@ struct RollVar {
     __device__ __forceinline__ double fresult(const Run& rn) const {
         return (rn.same >= W) ? 0.0 : divc<W - 1>(ssq);
     }
+    // warm add: the count n = nobs after the add (1 .. W) varies per lane while the window fills
+    __device__ __forceinline__ void wadd(const Step& s, double x, int n) {
+        double pm = mean - cadd, y = x - cadd, t = y - mean;
+        cadd = t + mean - y;
+        mean = mean + s.div(t, n);
+        ssq = ssq + (x - pm) * (x - mean);
+        nobs = n;
+    }
 };
 
 // ewm(adjust=False, ignore_na=False).mean(), minp = 1.  wtd starts NaN / old = 1, which
@@ -381,6 +390,14 @@ struct Ewm {
         wtd = (wtd != cur) ? num : wtd;
         return wtd;
     }
+    // warm step of a series observed on every present day from `first` on (cur finite there):
+    // before it wtd stays NaN, at it wtd = cur (pandas' first element), then the clean step
+    __device__ __forceinline__ double wstep(double cur, double owf, double nw, int p, int first) {
+        const double num = owf * wtd + nw * cur;
+        const double f = (wtd != cur) ? num : wtd;
+        wtd = p > first ? f : (p == first ? cur : wtd);
+        return wtd;
+    }
 };
 
 // alpha = 1 / (1 + com) exactly as pandas computes it (constant-folded in IEEE double)
@@ -414,6 +431,11 @@ struct Sma {  // No-talib.py:9-10
         m.fadd(s.C(0));
         s.putf((W - 6) / 4, m.fresult_pos<W>(s.rn->C));
     }
+    __device__ void wstep(Step& s) {
+        m.wstep(s.p >= W ? s.C(W) : 0.0, s.C(0), s.p >= W ? W : s.p + 1);
+        const double r = m.fresult_pos<W>(s.rn->C);
+        s.putf((W - 6) / 4, s.p >= W - 1 ? r : qnan());
+    }
 };
 
 template <int W>
@@ -425,6 +447,9 @@ struct Ema {  // No-talib.py:13-14
     }
     __device__ void fstep(Step& s) {
         s.putf(12 + (W - 6) / 4, e.fstep(s.C(0), SpanC<W>::owf, SpanC<W>::alpha));
+    }
+    __device__ void wstep(Step& s) {
+        s.putf(12 + (W - 6) / 4, e.wstep(s.C(0), SpanC<W>::owf, SpanC<W>::alpha, s.p, 0));
     }
 };
 
@@ -451,6 +476,16 @@ struct Vwma {  // No-talib.py:17-19
         mv.fadd(s.V(0));
         // a volume mean can round to 0 -> track
         s.put(24 + (W - 6) / 4, mvc.fresult_pos<W>(s.rn->VC) / mv.fresult_pos<W>(s.rn->V));
+    }
+    __device__ void wstep(Step& s) {
+        const bool rm = s.p >= W;
+        const int n = rm ? W : s.p + 1;
+        const double vq = rm ? s.V(W) : 0.0, cq = rm ? s.C(W) : 0.0;
+        const double v0 = s.V(0);
+        mvc.wstep(vq * cq, v0 * s.C(0), n);
+        mv.wstep(vq, v0, n);
+        const double r = mvc.fresult_pos<W>(s.rn->VC) / mv.fresult_pos<W>(s.rn->V);
+        s.put(24 + (W - 6) / 4, s.p >= W - 1 ? r : qnan());
     }
 };
 
@@ -484,6 +519,18 @@ struct Bbands {  // No-talib.py:22-26
         s.putf(col, ma + (2 * sd));
         s.putf(col + 1, ma - (2 * sd));
     }
+    __device__ void wstep(Step& s) {
+        const bool rm = s.p >= W;
+        const double x = s.C(0);
+        m.wstep(rm ? s.C(W) : 0.0, x, rm ? W : s.p + 1);
+        if (rm) v.fremove<W>(s.C(W));
+        v.wadd(s, x, rm ? W : s.p + 1);
+        const double ma = m.fresult_pos<W>(s.rn->C), sd = zsqrt(v.fresult<W>(s.rn->C));
+        const bool full = s.p >= W - 1;
+        const int col = 36 + 2 * ((W - 14) / 6);
+        s.putf(col, full ? ma + (2 * sd) : qnan());
+        s.putf(col + 1, full ? ma - (2 * sd) : qnan());
+    }
 };
 
 template <int W>
@@ -510,6 +557,14 @@ struct MomAccelRocr {  // No-talib.py:35-44
         s.putf(60 + k, mom - (s.C(1) - s.C(1 + W)));
         s.putf(68 + k, c / cw - 1);
     }
+    __device__ void wstep(Step& s) {
+        const int k = (W - 14) / 6;
+        const double c = s.C(0), cw = s.C(W);
+        const double mom = c - cw;
+        s.putf(52 + k, s.p >= W ? mom : qnan());
+        s.putf(60 + k, s.p >= W + 1 ? mom - (s.C(1) - s.C(1 + W)) : qnan());
+        s.putf(68 + k, s.p >= W ? c / cw - 1 : qnan());
+    }
 };
 
 template <int SLOW>
@@ -526,6 +581,12 @@ struct Macd {  // No-talib.py:47-50
         const double c = s.C(0);
         const double f = fast.fstep(c, SpanC<12>::owf, SpanC<12>::alpha);
         const double l = slow.fstep(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha);
+        s.putf(76 + (SLOW - 18) / 6, f - l);
+    }
+    __device__ void wstep(Step& s) {
+        const double c = s.C(0);
+        const double f = fast.wstep(c, SpanC<12>::owf, SpanC<12>::alpha, s.p, 0);
+        const double l = slow.wstep(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha, s.p, 0);
         s.putf(76 + (SLOW - 18) / 6, f - l);
     }
 };
@@ -552,6 +613,16 @@ struct Rsi {  // No-talib.py:53-59
         const double ed = dn.fstep(w, ComC<I - 1>::owf, ComC<I - 1>::alpha);
         const double rs = eu / ed;
         s.put(79 + (I - 8) / 6, 100 - (100 / (1 + rs)));     // 0 / 0 on flat prices -> track
+    }
+    // the up / down moves are observed from p = 1 (day 0's diff is NaN: both ewms stay NaN)
+    __device__ void wstep(Step& s) {
+        const double d = s.C(0) - s.C(1);
+        const double u = d >= 0 ? d : 0.0;
+        const double w = -(d <= 0 ? d : 0.0);
+        const double eu = up.wstep(u, ComC<I - 1>::owf, ComC<I - 1>::alpha, s.p, 1);
+        const double ed = dn.wstep(w, ComC<I - 1>::owf, ComC<I - 1>::alpha, s.p, 1);
+        const double rs = eu / ed;
+        s.put(79 + (I - 8) / 6, 100 - (100 / (1 + rs)));
     }
 };
 
@@ -585,6 +656,17 @@ struct PvtObvPsy {  // No-talib.py:62-69
         ups += (c > c1 ? 1 : 0) - (s.C(14) > s.C(15) ? 1 : 0);
         s.putf(84, divc<14>((double)ups) * 100);
     }
+    __device__ void wstep(Step& s) {
+        const int p = s.p;
+        const double c = s.C(0), v = s.V(0), c1 = s.C(1);
+        const double pv = pvt + v * (c / c1 - 1);
+        pvt = p >= 1 ? pv : pvt;
+        s.put(82, p >= 1 ? pvt : qnan());
+        obv = obv + v * ((p >= 1 && c - c1 <= 0) ? -1.0 : 1.0);   // day 0: NaN diff -> +volume
+        s.put(83, obv);
+        ups += (p >= 1 && c > c1 ? 1 : 0) - (p >= 15 && s.C(14) > s.C(15) ? 1 : 0);
+        s.putf(84, p >= 13 ? divc<14>((double)ups) * 100 : qnan());
+    }
 };
 
 template <int W, int COL>
@@ -605,6 +687,14 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
         s.putf(COL, r);
         return r;
     }
+    // returns start at p = 1: the window holds min(p, W) of them, the first remove is at W + 1
+    __device__ double wstep(Step& s) {
+        if (s.p >= W + 1) v.fremove<W>(s.fret(W));
+        if (s.p >= 1) v.wadd(s, s.r0, s.p >= W ? W : s.p);
+        const double r = s.p >= W ? zsqrt(v.fresult<W>(s.rn->R)) : qnan();
+        s.putf(COL, r);
+        return r;
+    }
 };
 
 struct RetSd3 {
@@ -612,6 +702,7 @@ struct RetSd3 {
     __device__ void init() { a.init(); }
     __device__ void step(Step& s) { a.step(s); }
     __device__ void fstep(Step& s) { a.fstep(s); }
+    __device__ void wstep(Step& s) { a.wstep(s); }
 };
 
 struct RetSd5x15 {  // sd_5, sd_15, sd5_15
@@ -624,6 +715,10 @@ struct RetSd5x15 {  // sd_5, sd_15, sd5_15
     }
     __device__ void fstep(Step& s) {
         double x = a.fstep(s), y = b.fstep(s);
+        s.put(88, x / y);
+    }
+    __device__ void wstep(Step& s) {
+        double x = a.wstep(s), y = b.wstep(s);
         s.put(88, x / y);
     }
 };
@@ -646,6 +741,13 @@ struct VolSd {  // volsd_W (No-talib.py:79-80)
         s.putf(COL, r);
         return r;
     }
+    __device__ double wstep(Step& s) {
+        if (s.p >= W) v.fremove<W>(s.V(W));
+        v.wadd(s, s.V(0), s.p >= W ? W : s.p + 1);
+        const double r = s.p >= W - 1 ? zsqrt(v.fresult<W>(s.rn->VP)) : qnan();
+        s.putf(COL, r);
+        return r;
+    }
 };
 
 struct VolSd3 {
@@ -653,6 +755,7 @@ struct VolSd3 {
     __device__ void init() { a.init(); }
     __device__ void step(Step& s) { a.step(s); }
     __device__ void fstep(Step& s) { a.fstep(s); }
+    __device__ void wstep(Step& s) { a.wstep(s); }
 };
 
 struct VolSd5x15 {
@@ -665,6 +768,10 @@ struct VolSd5x15 {
     }
     __device__ void fstep(Step& s) {
         double x = a.fstep(s), y = b.fstep(s);
+        s.put(92, x / y);
+    }
+    __device__ void wstep(Step& s) {
+        double x = a.wstep(s), y = b.wstep(s);
         s.put(92, x / y);
     }
 };
@@ -735,6 +842,35 @@ struct Corr {
         s.put(94 + (W == 15 ? 1 : 0), num / den);
         if (WITH_VC) s.putf(93, Y);
     }
+    // the pair starts at p = 1 (day 0's returns are NaN): min(p, W) pairs in the window, the
+    // first remove at W + 1; removes of 0 before it are exact no-ops on the Kahan means
+    __device__ void wstep(Step& s) {
+        const bool rm = s.p >= W + 1, ad = s.p >= 1;
+        const int n = s.p >= W ? W : s.p;
+        const double Xr = rm ? s.fret(W) : 0.0, Yr = rm ? s.fvolchg(W) : 0.0;
+        const double X = ad ? s.r0 : 0.0, Y = ad ? s.g0 : 0.0;
+        const double XYr = Xr * Yr, XY = X * Y;
+        mxy.wstep(XYr, XY, n);
+        mx.wstep(Xr, X, n);
+        my.wstep(Yr, Y, n);
+        if (rm) {
+            vx.fremove<W>(Xr);
+            vy.fremove<W>(Yr);
+        }
+        if (ad) {
+            vx.wadd(s, X, n);
+            vy.wadd(s, Y, n);
+        }
+        mxy.fsigns(XY, XYr);
+        mx.fsigns(X, Xr);
+        my.fsigns(Y, Yr);
+        cnt = n;
+        constexpr double cf = (double)W / (double)(W - 1);
+        const double num = (mxy.fresult<W>(s.rn->XY) - mx.fresult<W>(s.rn->X) * my.fresult<W>(s.rn->Y)) * cf;
+        const double den = __builtin_sqrt(vx.fresult<W>(s.rn->X) * vy.fresult<W>(s.rn->Y));
+        s.put(94 + (W == 15 ? 1 : 0), s.p >= W ? num / den : qnan());
+        if (WITH_VC) s.putf(93, ad ? s.g0 : qnan());
+    }
 };
 
 // ---- job packs ------------------------------------------------------------------------------
@@ -760,6 +896,7 @@ struct Pack<> {
     __device__ void init() {}
     __device__ void step(Step&) {}
     __device__ void fstep(Step&) {}
+    __device__ void wstep(Step&) {}
 };
 template <class H, class... R>
 struct Pack<H, R...> {
@@ -772,6 +909,7 @@ struct Pack<H, R...> {
         h.fstep(s);     // no scheduling barrier: the compiler interleaves the jobs' independent
         r.fstep(s);     // chains (12.55 -> 12.32 ms at config C, bit-identical)
     }
+    __device__ void wstep(Step& s) { h.wstep(s); r.wstep(s); }
 };
 
 // Static job partition over the 15 job waves of one workgroup (LPT on the per-job VALU count of
@@ -809,7 +947,8 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
     double pc[kChunk], pv[kChunk];
     u64 vb = a.vbits[(int64_t)((c0 * kChunk) >> 6) * a.lda + asset];
     int pmod = 0;                                   // observations before the staged chunk, mod kRing
-    int run = 0;                                    // consecutive in-range observations
+    int run = 0;                                    // consecutive in-range observations (cap kClean)
+    int cnt = 0;                                    // observations (capped at kClean)
     if (st && a.load_state) {                       // the ring and counters of the previous slab
         for (int q = 0; q < kRing; ++q) {
             sm.c[q][lane] = st[(2 * q) * kLanes + lane];
@@ -817,6 +956,7 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         }
         pmod = (int)st[(2 * kRing) * kLanes + lane];
         run = (int)st[(2 * kRing + 1) * kLanes + lane];
+        cnt = (int)st[(2 * kRing + 2) * kLanes + lane];
     }
     auto load = [&](int ch) {
 #pragma unroll
@@ -832,7 +972,7 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         if (sh == 0 && ch > c0) vb = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
         const u64 cb = (vb >> sh) & 0xffull;
         int q = pmod;
-        bool ok = true;
+        bool ok = true, warm = true;
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
             if ((cb >> j) & 1ull) {
@@ -840,13 +980,15 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
                 sm.v[q][lane] = pv[j];
                 q = q + 1 == kRing ? 0 : q + 1;
                 const bool good = pc[j] > kLo && pc[j] < kHi && pv[j] > kLo && pv[j] < kHi;
-                run = good ? run + 1 : 0;
+                run = good ? (run < kClean ? run + 1 : kClean) : 0;
+                cnt = cnt < kClean ? cnt + 1 : kClean;
                 ok = ok && run >= kClean;
+                warm = warm && (run >= kClean || run == cnt);   // every observation so far good
             }
         }
         pmod = q;
         sm.cbyte[ch & 1][lane] = (int)cb;
-        sm.okbyte[ch & 1][lane] = (a.fast && ok) ? 1 : 0;
+        sm.okbyte[ch & 1][lane] = !a.fast ? 0 : ok ? 2 : warm ? 1 : 0;
     };
     load(c0);
     stage(c0);
@@ -868,6 +1010,7 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         }
         st[(2 * kRing) * kLanes + lane] = (double)pmod;
         st[(2 * kRing + 1) * kLanes + lane] = (double)run;
+        st[(2 * kRing + 2) * kLanes + lane] = (double)cnt;
     }
 }
 
@@ -936,7 +1079,9 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     for (int ch = c0; ch < nch; ++ch) {
         const int sh = (ch * kChunk) & 63;                 // chunk offset inside its word
         const u64 cb = (u64)(unsigned)sm.cbyte[ch & 1][lane];
-        const bool clean = __builtin_amdgcn_ballot_w64(sm.okbyte[ch & 1][lane] == 0) == 0ull;
+        const int okl = sm.okbyte[ch & 1][lane];
+        const bool clean = __builtin_amdgcn_ballot_w64(okl != 2) == 0ull;
+        const bool warm = __builtin_amdgcn_ballot_w64(okl == 0) == 0ull;
         const int64_t t0 = (int64_t)ch * kChunk;
         int p = pos, pm = pmod;
         Step st;
@@ -954,11 +1099,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                 st.anynan = false;
                 st.anybad = false;
                 const double c0 = st.C(0), v0 = st.V(0);
-#ifdef AFM_FP_NOFASTCODE
-                if (false) {
-#else
                 if (clean) {
-#endif
                     if (S & (kSerR | kSerXY)) st.r0 = c0 / st.C(1) - 1;
                     if (S & kSerXY) st.g0 = v0 / st.V(1) - 1;
                     if (S & kSerC) rn.C.fupd(c0);
@@ -972,6 +1113,28 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                         rn.XY.fupd(st.r0 * st.g0);
                     }
                     jobs.fstep(st);
+                } else if (warm) {
+                    // warm-up windows: every observation of the lane so far in range (the first
+                    // kClean of a listing); the fast cores with the counts of a filling window.
+                    // Before p = 57 the row holds NaN (ACCEL_56), so the masks need no per-column
+                    // tracking there; from p = 57 the lane is clean and the fast columns' own
+                    // tracking applies.
+                    st.r0 = c0 / st.C(1) - 1;      // day 0: unused (no return yet)
+                    st.g0 = v0 / st.V(1) - 1;
+                    st.anynan = st.anybad = p < kClean - 1;
+                    if (S & kSerC) rn.C.fupd(c0);
+                    if (S & kSerV) rn.V.fupd(v0);
+                    if (S & kSerVP) rn.VP.fupd(v0);
+                    if (S & kSerVC) rn.VC.fupd(v0 * c0);
+                    if (p >= 1) {
+                        if (S & kSerR) rn.R.fupd(st.r0);
+                        if (S & kSerXY) {
+                            rn.X.fupd(st.r0);
+                            rn.Y.fupd(st.g0);
+                            rn.XY.fupd(st.r0 * st.g0);
+                        }
+                    }
+                    jobs.wstep(st);
                 } else {
                     if (S & (kSerR | kSerXY)) {
                         const double r = c0 / st.C(1) - 1;
@@ -1056,7 +1219,7 @@ constexpr int kStateWords = cmax(cmax(cmax(cmax(state_words<W0>(), state_words<W
     cmax(state_words<W2>(), state_words<W3>())), cmax(cmax(state_words<W4>(), state_words<W5>()),
     cmax(state_words<W6>(), state_words<W7>()))), cmax(cmax(cmax(state_words<W8>(),
     state_words<W9>()), cmax(state_words<W10>(), state_words<W11>())), cmax(cmax(
-    state_words<W12>(), state_words<W13>()), cmax(state_words<W14>(), 2 * kRing + 2))));
+    state_words<W12>(), state_words<W13>()), cmax(state_words<W14>(), 2 * kRing + 3))));
 
 // TYPES workgroups per block, each with J = 15 / TYPES job waves (job sets W[J*type + wave]) and
 // a loader wave.  PAIR: one workgroup runs TWO such items (two rings, 2 x (J + 1) waves), items
@@ -1075,7 +1238,7 @@ __constant__ signed char kPairLayout[3][2][6] = {
 };
 
 template <int TYPES, bool PAIR>
-__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1) * (PAIR ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(TYPES == 1 ? 4 : TYPES == 3 ? AFM_FP_WPE3 : 2)))
+__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1) * (PAIR ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(TYPES == 1 ? 4 : TYPES == 3 ? 3 : 2)))
 void factor_panel_kernel(Args a) {
     constexpr int J = kJobSets / TYPES;
     // dynamic LDS: with a static size the compiler pads the VGPR allocation of the split
@@ -1115,10 +1278,6 @@ void factor_panel_kernel(Args a) {
 #ifdef AFM_FP_PROFILE
     at.pslot = (int)(block * TYPES + type);          // profile slot of this item
 #endif
-#ifdef AFM_FP_ONLY
-    run_wave<AFM_FP_ONLY>(at, sm, 0, wave, lane, block, stp);
-    return;
-#endif
     switch (type * J + wave) {
         case 0: run_wave<W0>(at, sm, 0, wave, lane, block, stp); break;
         case 1: run_wave<W1>(at, sm, 0, wave, lane, block, stp); break;
@@ -1157,37 +1316,58 @@ __global__ __launch_bounds__(256) void masks_kernel(int64_t nwords, int64_t lda,
 }
 
 // target = excess_ret1d.shift(-1), tmr_ret1d = ret1d.shift(-1) (No-talib.py:90-91): the value of
-// the asset's NEXT present day, NaN on its last one.  One thread per cell, next present day found
-// from the presence words (ctz), rows read/written coalesced.
+// the asset's NEXT present day, NaN on its last one.  One thread per (asset, 64-day presence
+// word): the word is walked backwards carrying the next present day's pair, so every load and
+// store is a coalesced row segment (lanes = consecutive assets, one date) and the loads of a
+// 16-day group are issued together.  The pair that enters a word from the right is the first
+// present day of a later word.  Only present cells of [t_begin, t_end) are written.
 __global__ __launch_bounds__(256) void labels_kernel(int64_t T, int64_t t_begin, int64_t t_end,
                                                      int64_t lda, const double* excess,
                                                      const double* ret1d, const uint64_t* vbits,
                                                      double* target, double* tmr) {
-    const int64_t a = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-    const int64_t t = t_begin + (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (t >= t_end) return;
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (a >= lda) return;
+    const int64_t c = (t_begin >> 6) + blockIdx.y;
     const int64_t nch = (T + 63) / 64;
-    int64_t ch = t >> 6;
-    const int s = (int)(t & 63);
-    u64 w = vbits[ch * lda + a];
-    if (!((w >> s) & 1ull)) return;
-    u64 rest = (s == 63) ? 0ull : (w >> (s + 1)) << (s + 1);
-    int64_t tn = -1;
-    while (true) {
-        if (rest) {
-            tn = ch * 64 + __builtin_ctzll(rest);
+    const u64 w = vbits[c * lda + a];
+    if (!w) return;
+    // the first present day after this word
+    double ne = __builtin_nan(""), nr = __builtin_nan("");
+    for (int64_t cc = c + 1; cc < nch; ++cc) {
+        const u64 x = vbits[cc * lda + a];
+        if (x) {
+            const int64_t tn = cc * 64 + __builtin_ctzll(x);
+            ne = excess[tn * lda + a];
+            nr = ret1d[tn * lda + a];
             break;
         }
-        if (++ch >= nch) break;
-        rest = vbits[ch * lda + a];
     }
-    const int64_t cell = t * lda + a;
-    if (tn >= 0 && tn < T) {
-        target[cell] = excess[tn * lda + a];
-        tmr[cell] = ret1d[tn * lda + a];
-    } else {
-        target[cell] = __builtin_nan("");
-        tmr[cell] = __builtin_nan("");
+    const int64_t d0 = c * 64;
+    const int s_lo = t_begin > d0 ? (int)(t_begin - d0) : 0;
+    const int s_hi = t_end - d0 < 64 ? (int)(t_end - d0) : 64;     // write [s_lo, s_hi)
+    for (int g = 48; g >= 0; g -= 16) {
+        if (!((w >> g) & 0xffffull)) continue;
+        double e[16], r[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {                // rows past T are never present
+            const int64_t t = d0 + g + j;
+            const int64_t tc = t < T ? t : T - 1;
+            e[j] = excess[tc * lda + a];
+            r[j] = ret1d[tc * lda + a];
+        }
+#pragma unroll
+        for (int j = 15; j >= 0; --j) {
+            const int s = g + j;
+            if ((w >> s) & 1ull) {
+                if (s >= s_lo && s < s_hi) {
+                    const int64_t cell = (d0 + s) * lda + a;
+                    target[cell] = ne;
+                    tmr[cell] = nr;
+                }
+                ne = e[j];
+                nr = r[j];
+            }
+        }
     }
 }
 
@@ -1232,10 +1412,7 @@ static int factor_types(afm_ctx* ctx, int64_t nblk) {
     int types = 3;
     for (int t : {5, 15})
         if (nblk * t <= 2 * (int64_t)ncu) types = t;
-    if (const char* e = getenv("AFM_FP_TYPES")) {                 // tuning override
-        const int t = atoi(e);
-        if (t == 1 || t == 3 || t == 5 || t == 15) types = t;
-    }
+    if (ctx->factor_split) types = ctx->factor_split;              // option factor_split
     return types;
 }
 
@@ -1271,46 +1448,18 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     a.t1 = t1;
     a.state = (GLB double*)state;
     a.load_state = t0 > 0 ? 1 : 0;
-    // paired 12-wave workgroups for the 3-way split (see factor_panel_kernel); AFM_FP_PAIR=0: A/B
-    bool pair = true;
-    if (const char* e = getenv("AFM_FP_PAIR")) pair = atoi(e) != 0;
-    if (const char* e = getenv("AFM_FP_NOFAST"))                   // A/B: general step only
-        a.fast = atoi(e) ? 0 : 1;
+    // paired 12-wave workgroups for the 3-way split (see factor_panel_kernel); options
+    // factor_pair / factor_fast: the invariance tests' A/B
+    const bool pair = ctx->factor_pair != 0;
+    a.fast = ctx->factor_fast ? 1 : 0;
     const dim3 grid((unsigned)(nblk * types));
-    static bool layout_set = false;                   // tuning override of kPairLayout:
-    if (!layout_set) {                                // 36 digits, [type][half][position]
-        layout_set = true;
-        if (const char* e = getenv("AFM_FP_LAYOUT")) {
-            signed char l[36];
-            int n = 0;
-            for (; e[n] && n < 36; ++n) l[n] = (signed char)(e[n] - '0');
-            bool ok = n == 36 && e[n] == 0;
-            for (int h = 0; ok && h < 6; ++h) {           // each (type, half): a permutation of 0..5
-                int seen = 0;
-                for (int q = 0; q < 6; ++q) {
-                    const int v = l[6 * h + q];
-                    if (v < 0 || v > 5 || (seen >> v) & 1) ok = false;
-                    else seen |= 1 << v;
-                }
-            }
-            AFM_CHECK_ARG(ok, "AFM_FP_LAYOUT: 36 digits, each group of 6 a permutation of 0..5");
-            AFM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(afm::kPairLayout), l, sizeof(l)));
-        }
-    }
-    static bool lds_attr = false;                     // > 64 KB of dynamic LDS: opt in once
-    if (!lds_attr) {
+    {                                                 // > 64 KB of dynamic LDS: opt in
         const int bytes = (int)sizeof(afm::Smem);
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<1, false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<3, false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<3, true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 2 * bytes));
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<5, false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::factor_panel_kernel<15, false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-        lds_attr = true;
+        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<1, false>, bytes));
+        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<3, false>, bytes));
+        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<3, true>, 2 * bytes));
+        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<5, false>, bytes));
+        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<15, false>, bytes));
     }
     switch (types) {
         case 1: hipLaunchKernelGGL((afm::factor_panel_kernel<1, false>), grid, dim3(64 * 16),
@@ -1338,7 +1487,7 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
                        part + types * nw, nanfree_bits, finite_bits);
     AFM_HIP(hipGetLastError());
     if (excess) {                  // NULL: the caller runs afm_labels_f64 (e.g. on another stream)
-        dim3 g2((unsigned)(lda / 64), (unsigned)((t1 - t0 + 3) / 4));
+        dim3 g2((unsigned)((lda + 255) / 256), (unsigned)((t1 - 1) / 64 - t0 / 64 + 1));
         hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, t0, t1, lda,
                            excess, ret1d, valid_bits, out + 96 * a.plane - t0 * lda,
                            out + 97 * a.plane - t0 * lda);
@@ -1398,7 +1547,7 @@ extern "C" int afm_labels_f64(afm_ctx* ctx, int64_t T, int64_t lda, int64_t t0, 
     t0 = t0 < 0 ? 0 : t0;
     t1 = t1 > T ? T : t1;
     if (t1 <= t0) return AFM_OK;
-    dim3 g2((unsigned)(lda / 64), (unsigned)((t1 - t0 + 3) / 4));
+    dim3 g2((unsigned)((lda + 255) / 256), (unsigned)((t1 - 1) / 64 - t0 / 64 + 1));
     hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, t0, t1, lda, excess,
                        ret1d, valid_bits, target, tmr);
     AFM_HIP(hipGetLastError());

@@ -153,13 +153,7 @@ extern "C" int afm_lasso_cd_f64(afm_ctx* ctx, const double* gram, int p, double 
     AFM_CHECK_ARG(max_iter >= 1, "max_iter must be >= 1");
     AFM_CHECK_ARG(alpha_n >= 0 && beta >= 0 && tol >= 0, "alpha, beta and tol must be >= 0");
     const int lds = (int)sizeof(double) * p * p;
-    static bool attr = false;
-    if (!attr) {
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::lasso_cd_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
-        attr = true;
-    }
+    AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::lasso_cd_kernel, (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
     hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(afm::kLassoThreads), lds, ctx->stream,
                        gram, p, alpha_n, beta, max_iter, tol, positive, w, info, -1.0,
                        (const double*)nullptr, (double*)nullptr);
@@ -175,13 +169,7 @@ extern "C" int afm_lasso_fit_f64(afm_ctx* ctx, const double* gram, const double*
     AFM_CHECK_ARG(gram && shift && beta_out && info, "null buffer");
     AFM_CHECK_ARG(max_iter >= 1 && alpha >= 0 && tol >= 0, "bad max_iter / alpha / tol");
     const int lds = (int)sizeof(double) * p * p;
-    static bool attr = false;
-    if (!attr) {
-        AFM_HIP(hipFuncSetAttribute((const void*)afm::lasso_cd_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
-        attr = true;
-    }
+    AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::lasso_cd_kernel, (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
     hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(afm::kLassoThreads), lds, ctx->stream,
                        gram, p, 0.0, 0.0, max_iter, tol, positive, (double*)nullptr, info, alpha, shift,
                        beta_out);

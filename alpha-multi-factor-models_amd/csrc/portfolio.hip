@@ -1335,8 +1335,7 @@ using namespace afm;
 template <int KM>
 static int launch_rebalance(afm_ctx* ctx, const RebArgs& r) {
     const size_t smem = sizeof(Shared<KM>);
-    AFM_HIP(hipFuncSetAttribute((const void*)rebalance_kernel<KM>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    AFM_HIP(afm_lds_opt_in(ctx, (const void*)rebalance_kernel<KM>, (int)smem));
     hipLaunchKernelGGL(rebalance_kernel<KM>, dim3((unsigned)r.nd, 2), dim3(kT), smem, ctx->stream,
                        r);
     AFM_HIP(hipGetLastError());
@@ -1369,7 +1368,9 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
                                ctx->stream));
     RebArgs r{T, lda, A, dates, nd, pred, trad_bits, hist, hist_bits, h_t0, h_t1, window, close,
               tmr, top_n, lo, hi, hscr, hrows, 0, nullptr, k_out, books, weights, sums, upos, usize, status};
+#ifdef AFM_PROBE                     // profiling build (make prof): phase experiments
     if (const char* e = getenv("AFM_REB_PROBE")) r.probe = atoi(e);
+#endif
     if (r.probe & 4) AFM_HIP(hipMallocAsync((void**)&r.stamps, sizeof(int64_t) * nd * 16, ctx->stream));
     const int rc = top_n <= 32 ? launch_rebalance<32>(ctx, r) : launch_rebalance<kMaxK>(ctx, r);
     if (r.stamps) {                  // experiment: mean phase durations per workgroup
@@ -1423,8 +1424,7 @@ extern "C" int afm_min_variance_weights_f64(afm_ctx* ctx, const double* R, int64
     AFM_CHECK_ARG(k >= 1 && k <= kMaxK && ld >= k && rows >= 0, "need 1 <= k <= 128, ld >= k");
     AFM_CHECK_ARG(R && w && cov && status && lo <= hi, "bad arguments");
     const size_t smem = sizeof(Shared<kMaxK>);
-    AFM_HIP(hipFuncSetAttribute((const void*)weights_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    AFM_HIP(afm_lds_opt_in(ctx, (const void*)weights_kernel, (int)smem));
     hipLaunchKernelGGL(weights_kernel, dim3(1), dim3(kT), smem, ctx->stream, R, rows, ld, k, lo,
                        hi, w, cov, status);
     AFM_HIP(hipGetLastError());

@@ -1041,9 +1041,8 @@ extern "C" int afm_xs_gram_f64(afm_ctx* ctx, const double* base, int64_t col_str
     GramArgs g{base, col_stride, seg_stride, seg_rows, row_limit, cols, ycol, p, bits, seg0, gram,
                shift};
     const int nt = (p + 15) / 16;
-    // AFM_GRAM_CHECKED=1: the checked staging only (A/B tests)
-    const char* ce = getenv("AFM_GRAM_CHECKED");
-    const bool checked = ce && atoi(ce) != 0;
+    // option gram_checked: the checked staging only (A/B tests)
+    const bool checked = ctx->gram_checked != 0;
     for (const int mode : {checked ? 0 : 1, checked ? -1 : 2}) {
         if (mode < 0) break;
         AFM_HIP(launch_gram(nt, mode, dim3((unsigned)nseg), ctx->stream, g));
@@ -1060,8 +1059,7 @@ extern "C" int afm_ols_solve_f64(afm_ctx* ctx, const double* gram, const double*
     if (nseg <= 0) return AFM_OK;
     SolveArgs s{gram, shift, p, tol, nullptr, p, beta, nobs, rank};
     const size_t lds = sizeof(double) * (size_t)(p + 1) * (p + 2) / 2;     // packed triangle
-    AFM_HIP(hipFuncSetAttribute((const void*)ols_solve_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    AFM_HIP(afm_lds_opt_in(ctx, (const void*)ols_solve_kernel, (int)lds));
     hipLaunchKernelGGL(ols_solve_kernel, dim3((unsigned)nseg), dim3(kThreads), lds, ctx->stream,
                        s);
     AFM_HIP(hipGetLastError());

@@ -189,13 +189,8 @@ struct Seq {
 // ahead, issued before the newer x loads (loads retire in order); mode 1 once per item -- the
 // item keeps its 64 assets, so the row-block's statistics stay in registers across its dates.
 // z = (x - mu) * rsig; masked-out rows stage exact zeros.
-#ifndef AFM_ZG_TPL
-#define AFM_ZG_TPL 0
-#endif
-template <int NT, int MODE, bool ZS, int PW>
-__device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, const int pw_rt) {
-    // AFM_ZG_TPL: the wave index as a compile-time constant (immediate LDS offsets) or not
-    const int pw = AFM_ZG_TPL ? PW : pw_rt;
+template <int NT, int MODE, bool ZS>
+__device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, const int pw) {
     constexpr int MC = ZCfg<NT>::MC;
     const int p = g.p;
     const int K = p + 2;
@@ -242,18 +237,11 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, con
         B.ok = in && ((g.bits[(int64_t)(t >> 6) * lda + ac] >> (t & 63)) & 1ull);
         B.zoff = (unsigned)ac * 16u;
         B.item = cur.item;
-#if defined(AFM_ZG_SKIP) && AFM_ZG_SKIP == 2              // experiments: consumers alone
-        B.ok = false;
-        return;
-#endif
         const unsigned off = (unsigned)(t * lda + ac) * 8u;
 #pragma unroll
         for (int j = 0; j < MC; ++j) B.x[j] = *reinterpret_cast<const double*>(xsrc(j) + off);
     };
     auto zload = [&](const unsigned zoff) {
-#if defined(AFM_ZG_SKIP) && AFM_ZG_SKIP == 2
-        return;
-#endif
         if (!ZS) return;                             // raw columns: no statistics
 #pragma unroll
         for (int j = 0; j < MC; ++j) {
@@ -306,10 +294,8 @@ __device__ void zgram_produce(const ZGramArgs& g, ZSmem& sm, const int lane, con
 // Items have an even slot count (g.even), so each iteration stages the pair (A, C) of one item.
 // (The pooled Gram keeps zgram_produce: it is bound by the MFMA / staging serialisation on the
 // SIMDs, and there the deeper prefetch measured slower, 11.1 -> 12.1 ms.)
-template <int NT, int MODE, bool ZS, int PW>
-__device__ void zgram_produce_pairs(const ZGramArgs& g, ZSmem& sm, const int lane, const int pw_rt) {
-    // AFM_ZG_TPL: the wave index as a compile-time constant (immediate LDS offsets) or not
-    const int pw = AFM_ZG_TPL ? PW : pw_rt;
+template <int NT, int MODE, bool ZS>
+__device__ void zgram_produce_pairs(const ZGramArgs& g, ZSmem& sm, const int lane, const int pw) {
     constexpr int MC = ZCfg<NT>::MC;
     const int p = g.p;
     const int K = p + 2;
@@ -363,19 +349,12 @@ __device__ void zgram_produce_pairs(const ZGramArgs& g, ZSmem& sm, const int lan
         B.zoff = (unsigned)ac * 16u;
         B.word = reinterpret_cast<const uint32_t*>(g.bits)[((int64_t)(tl >> 6) * lda + ac) * 2 +
                                                            ((tl >> 5) & 1)];
-#if defined(AFM_ZG_SKIP) && AFM_ZG_SKIP == 2              // experiments: consumers alone
-        B.in = false;
-#else
         const unsigned off = (unsigned)(tl * lda + ac) * 8u;
 #pragma unroll
         for (int j = 0; j < MC; ++j) B.x[j] = *reinterpret_cast<const double*>(xsrc(j) + off);
-#endif
         if (v) cur.advance(g);
     };
     auto zload = [&](const unsigned zoff) {
-#if defined(AFM_ZG_SKIP) && AFM_ZG_SKIP == 2
-        return;
-#endif
         if (!ZS) return;                             // raw columns: no statistics
 #pragma unroll
         for (int j = 0; j < MC; ++j) {
@@ -450,35 +429,19 @@ __device__ void zgram_consume(const ZGramArgs& g, ZSmem& sm, const int lane) {
             for (int t = 0; t < THI; ++t) f[t] = tb[lrow[t] * kZRS + a];
         };
         auto step = [&](const double (&f)[NT]) {
-#if defined(AFM_ZG_SKIP) && AFM_ZG_SKIP == 1
-            return;
-#endif
 #pragma unroll
             for (int q = 0; q < NQ; ++q)
                 acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(f[tab.I[Q0 + q]], f[tab.J[Q0 + q]],
                                                               acc[q], 0, 0, 0);
         };
-        // k-step it+1's fragments are requested before k-step it's MFMAs (the sched barriers keep
-        // that order, so each wait covers only the older requests)
-#ifndef AFM_ZG_SB
-#define AFM_ZG_SB 0
-#endif
-#if AFM_ZG_SB
-#define ZG_SB() __builtin_amdgcn_sched_barrier(0)
-#else
-#define ZG_SB()
-#endif
+        // k-step it+1's fragments are requested before k-step it's MFMAs
         ld(fa, 0);
 #pragma unroll
         for (int it = 0; it < 16; it += 2) {
             ld(fb, it + 1);
-            ZG_SB();
             step(fa);
-            ZG_SB();
             if (it + 2 < 16) ld(fa, it + 2);
-            ZG_SB();
             step(fb);
-            ZG_SB();
         }
         signal_count(&sm.freed[slot], lane);
         if (++slot == sm.nslots) { slot = 0; ++gen; }
@@ -581,7 +544,7 @@ __device__ void zgram_border_any(const ZGramArgs& g, ZSmem& sm, const int lane) 
 }
 
 template <int NT, int MODE, bool ZS>
-__global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int nslots, int prio) {
+__global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int nslots) {
     extern __shared__ __attribute__((aligned(16))) double ring[];
     __shared__ ZSmem sm;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -597,23 +560,9 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
     if (tid < kZMaxSlots) { sm.ready[tid] = 0; sm.freed[tid] = 0; }
     __syncthreads();
     if (wave >= 4 && wave < 4 + kZProd) {
-        if (prio & 1) __builtin_amdgcn_s_setprio(1);
-        if (NT == 2) {
-            zgram_produce_pairs<NT, MODE, ZS, 0>(g, sm, lane, wave - 4);
-        } else if (!AFM_ZG_TPL) {
-            zgram_produce<NT, MODE, ZS, 0>(g, sm, lane, wave - 4);
-        } else {
-            switch (wave - 4) {
-                case 0: zgram_produce<NT, MODE, ZS, 0>(g, sm, lane, 0); break;
-                case 1: zgram_produce<NT, MODE, ZS, 1>(g, sm, lane, 1); break;
-                case 2: zgram_produce<NT, MODE, ZS, 2>(g, sm, lane, 2); break;
-                case 3: zgram_produce<NT, MODE, ZS, 3>(g, sm, lane, 3); break;
-                case 4: zgram_produce<NT, MODE, ZS, 4>(g, sm, lane, 4); break;
-                case 5: zgram_produce<NT, MODE, ZS, 5>(g, sm, lane, 5); break;
-                case 6: zgram_produce<NT, MODE, ZS, 6>(g, sm, lane, 6); break;
-                default: zgram_produce<NT, MODE, ZS, 7>(g, sm, lane, 7); break;
-            }
-        }
+        __builtin_amdgcn_s_setprio(1);              // producers ahead of the MFMA consumers
+        if (NT == 2) zgram_produce_pairs<NT, MODE, ZS>(g, sm, lane, wave - 4);
+        else zgram_produce<NT, MODE, ZS>(g, sm, lane, wave - 4);
         return;
     }
     if (wave == 12) {
@@ -622,7 +571,6 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
         if constexpr (ZCfg<NT>::BORDER) zgram_border_any<NT>(g, sm, lane);
         return;
     }
-    if (prio & 2) __builtin_amdgcn_s_setprio(2);
     if (wave == 0) {
         zgram_consume<NT, 0>(g, sm, lane);
     } else if (wave == 1) {
@@ -681,11 +629,15 @@ __global__ __launch_bounds__(256) void zstats_finalize_kernel(const double* mu, 
     int ok = 1;
     for (int k = 0; k < K; ++k) {
         const double m = mu[(int64_t)k * lda + a], s = sd[(int64_t)k * lda + a];
-        const bool okk = __builtin_isfinite(m) && s > 0.0;       // NaN sigma fails s > 0
+        const double r = 1.0 / s;
+        // NaN sigma fails s > 0.  A subnormal sigma (< 2^-1024, 1/sigma overflows) also drops the
+        // asset: the reference's (x - mu) / sigma could stay finite there, the product form
+        // cannot ("z = (x - mu) * (1/sigma)").
+        const bool okk = __builtin_isfinite(m) && s > 0.0 && __builtin_isfinite(r);
         ok &= okk ? 1 : 0;
         double2 v;
         v.x = okk ? m : 0.0;
-        v.y = okk ? 1.0 / s : 0.0;
+        v.y = okk ? r : 0.0;
         reinterpret_cast<double2*>(zs)[(int64_t)k * lda + a] = v;
     }
     double2 one;
@@ -781,20 +733,9 @@ static int launch_zgram(afm_ctx* ctx, const ZGramArgs& g, int64_t nitems, int gr
     int nslots = kZLds / slot_bytes;
     if (nslots > kZMaxSlots) nslots = kZMaxSlots;
     AFM_CHECK_ARG(nslots >= 2, "ring does not fit in LDS");
-    static bool attr = false;
-    if (!attr) {
-        AFM_HIP(hipFuncSetAttribute((const void*)zgram_kernel<NT, MODE, ZS>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, kZLds));
-        attr = true;
-    }
-    // AFM_ZG_PRIO (experiments): bit 0 = producers at priority 1 (default), bit 1 = consumers at 2
-    static int prio = -1;
-    if (prio < 0) {
-        const char* e = getenv("AFM_ZG_PRIO");
-        prio = e ? atoi(e) : 1;
-    }
+    AFM_HIP(afm_lds_opt_in(ctx, (const void*)zgram_kernel<NT, MODE, ZS>, kZLds));
     hipLaunchKernelGGL((zgram_kernel<NT, MODE, ZS>), dim3((unsigned)wg), dim3(kZThreads),
-                       (size_t)nslots * slot_bytes, ctx->stream, g, nslots, prio);
+                       (size_t)nslots * slot_bytes, ctx->stream, g, nslots);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

@@ -40,6 +40,13 @@ typedef struct afm_ctx afm_ctx;
 int afm_ctx_create(int device, afm_ctx** out);
 /* stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = default stream */
 int afm_ctx_set_stream(afm_ctx* ctx, void* stream);
+/* Execution options of a context -- work splits that never change a result (the invariance tests
+ * set them; defaults are the library's choice):
+ *   "factor_split"  0 (auto) | 1 | 3 | 5 | 15: workgroups per 64-asset block of the factor kernel
+ *   "factor_pair"   1 (default) | 0: the 3-way split runs two items per workgroup
+ *   "factor_fast"   1 (default) | 0: the clean-window fast step of the factor kernel
+ *   "gram_checked"  0 (default) | 1: afm_xs_gram_f64 stages every row checked (no FAST + REDO) */
+int afm_ctx_set_option(afm_ctx* ctx, const char* name, int64_t value);
 int afm_ctx_destroy(afm_ctx* ctx);
 const char* afm_last_error(void);
 int afm_version(void);

@@ -112,8 +112,11 @@ def _analyzer(pred, price, k_layers=10, top=10):
     return ic, lay.cumsum(), port
 
 
-def run_chain(p, train_end, valid_end, *, window=252, top_n=10, rate=1e-4, timings=None):
-    """The chain on synthetic panel ``p`` in the reference's call pattern; returns the value path."""
+def run_chain(p, train_end, valid_end, *, window=252, top_n=10, rate=1e-4, timings=None,
+              max_dates=None):
+    """The chain on synthetic panel ``p`` in the reference's call pattern; returns the value path.
+    ``max_dates``: stop the per-date PortfolioManager loop after that many rebalance dates (a
+    bounded timing sample; ``timings['dates']`` / ``['dates_total']`` say how many ran)."""
     import pandas as pd
     import scipy.optimize as sco
     from sklearn.linear_model import Lasso
@@ -162,9 +165,18 @@ def run_chain(p, train_end, valid_end, *, window=252, top_n=10, rate=1e-4, timin
                            constraints=({"type": "eq", "fun": lambda x: np.sum(x) - 1},))
         return res["x"]
 
-    for date, preds in pred.groupby(level="date"):
+    t_filter = 0.0
+    groups = pred.groupby(level="date")
+    tm["dates_total"] = groups.ngroups
+    tm["dates"] = 0
+    for date, preds in groups:
+        if max_dates is not None and tm["dates"] >= max_dates:
+            break
+        tm["dates"] += 1
         preds = preds.droplevel(0)
-        trad = all_df[all_df["in_trading_universe"] == "Y"].loc[date].index
+        tf = time.perf_counter()
+        trad = all_df[all_df["in_trading_universe"] == "Y"].loc[date].index     # KKT:847, O(panel)
+        t_filter += time.perf_counter() - tf
         ids = list(set(trad) & set(preds.index))
         k = len(ids) // 2 if len(ids) < 2 * top_n else top_n
         longs = preds.loc[ids].nlargest(k).index.tolist()
@@ -186,4 +198,5 @@ def run_chain(p, train_end, valid_end, *, window=252, top_n=10, rate=1e-4, timin
         value.append(value[-1] * (1 + r))
         cur = new
     tm["portfolio"] = time.perf_counter() - t4
+    tm["filter_847"] = t_filter                      # inside "portfolio": the per-date all_df filter
     return np.array(value)

@@ -4,7 +4,8 @@ against the oracle on sampled dates / paths (sizes where the whole oracle chain 
 * C (10,000 assets x 5,040 days, 96 factors, window 252, top_n 10): every date's k, status and
   weights; the value path recomputed on the host by the oracle's KKT:864-892 recursion from the
   engine's books and PnL components (bit-exact); books vs oracle.portfolio.select_books on 24
-  sampled dates from the engine's predictions.
+  sampled dates from the engine's predictions; the pooled Gram vs torch fp64 D^T D, the Lasso
+  vs the oracle's coordinate descent, predictions on 20 sampled dates.
 * B (3,000 assets x 5,040 days, FM30): per-date Fama-MacBeth betas vs the oracle's lstsq on the
   same rows (rel 1e-9) and the IC series vs the oracle analyzer (oracle/xs.py) on sampled dates.
 * E (1,024 bootstrap paths x 5,000 assets): sampled paths vs the oracle recursion over the same
@@ -78,6 +79,71 @@ def test_config_c_books_weights_value(config_c):
         ids = np.flatnonzero(~np.isnan(pred[t]))
         L, S = P.select_books(ids, pred[t, ids], trad[t, ids], top_n)
         assert np.array_equal(recs[i]["L"], L) and np.array_equal(recs[i]["S"], S), i
+
+
+def test_config_c_pooled_gram_lasso_predict(config_c):
+    """Config C's regression leg at full size (41 M pooled rows x 99 columns):
+    * the pooled Gram of [1, z_1..z_97, target] over train + valid (train_end twice, KKT:426-427)
+      against torch fp64 D^T D of the same z-scored rows (z = (x - mu) * (1/sigma), the
+      engine's zs), accumulated in 128-date chunks: rel 1e-12 of max |G|, the row count exact;
+    * the Lasso (KKT:605-607) against the oracle's Gram coordinate descent
+      (oracle/lasso_oracle.c, scikit-learn 1.7.2's algorithm) on the engine's Gram: coefficients
+      and iteration count bit-exact, and on the reference Gram: same support, rel 1e-9;
+    * lasso.predict (KKT:612) on 20 sampled test dates: b0 + sum_j b_j z_j in the engine's order
+      (ascending j, zero coefficients skipped) -- bit-exact, NaN off the z-score rows."""
+    import torch
+    import oracle
+    from afm.grid import unpack_bits
+    p, grid, pipe = config_c
+    sp, T, lda = pipe.sp, pipe.T, pipe.lda
+    zr = unpack_bits(pipe.zrows, T)                                     # [T][lda] bool
+    feat = pipe.feat.long()
+    mu, rs = pipe.zs[:pipe.p, :, 0], pipe.zs[:pipe.p, :, 1]
+    G = torch.zeros((pipe.p2, pipe.p2), dtype=torch.float64, device=pipe.out.device)
+
+    def add_rows(t0, t1):
+        tt, aa = torch.nonzero(zr[t0:t1], as_tuple=True)
+        if len(tt) == 0:
+            return torch.zeros_like(G)
+        X = pipe.out[feat, t0:t1][:, tt, aa]                           # [p][n]
+        Z = (X - mu[:, aa]) * rs[:, aa]
+        y = pipe.out[96, t0:t1][tt, aa]
+        D = torch.cat([torch.ones_like(y)[None], Z, y[None]], dim=0)
+        return D @ D.T
+
+    for t0 in range(0, sp.v1, 128):
+        G += add_rows(t0, min(sp.v1, t0 + 128))
+    if sp.dup:
+        G += add_rows(sp.tr1 - 1, sp.tr1)
+    got = pipe.pool_g[0]
+    assert got[0, 0].item() == G[0, 0].item() > 4e7
+    err = ((got - G).abs().max() / G.abs().max()).item()
+    assert err < 1e-12, err
+    # Lasso on the engine's Gram: the oracle's coordinate descent, bit for bit
+    c = pipe.cfg
+    n, Q, q, yy = oracle.centered_moments(got.cpu().numpy())
+    w, gap, tol_y, it = oracle.lasso_gram(Q, q, yy, c.alpha * n, max_iter=c.max_iter,
+                                          tol=c.lasso_tol)
+    b = pipe.lasso_beta.cpu().numpy()
+    assert np.array_equal(b[1:], w)
+    assert int(pipe.lasso_info[2].item()) == it
+    # ... and on the reference Gram: the same fit within rel 1e-9
+    n2, Q2, q2, yy2 = oracle.centered_moments(G.cpu().numpy())
+    w2, _, _, _ = oracle.lasso_gram(Q2, q2, yy2, c.alpha * n2, max_iter=c.max_iter, tol=c.lasso_tol)
+    assert np.array_equal(w2 != 0, w != 0)
+    assert np.abs(w2 - w).max() <= 1e-9 * np.abs(w).max()
+    # predictions on sampled test dates
+    pred = pipe.pred
+    nz = np.flatnonzero(b[1:] != 0)
+    for t in np.linspace(sp.s0, T - 2, 20).astype(int):
+        m = zr[t]
+        aa = torch.nonzero(m).flatten()
+        s = torch.full((len(aa),), b[0], dtype=torch.float64, device=pred.device)
+        for j in nz:
+            z = (pipe.out[feat[j], t, aa] - mu[j, aa]) * rs[j, aa]
+            s = s + b[1 + j] * z
+        assert torch.equal(pred[t, aa], s), t
+        assert torch.isnan(pred[t, ~m]).all(), t
 
 
 @pytest.fixture(scope="module")

@@ -61,18 +61,18 @@ def test_factor_grid_vs_oracle(A, T, seed, kw):
                                           ("3", "0", 200), ("5", "1", 200), ("15", "1", 200)])
 def test_factor_workgroup_splits_identical(types, pair, A, monkeypatch):
     """Every split of a block's 15 job waves over 1, 3, 5 or 15 workgroups (chosen from the
-    shard's block count; AFM_FP_TYPES overrides), paired two items per workgroup or not
-    (AFM_FP_PAIR; A = 300 leaves the last pair half idle), gives the same bit-exact panel and
-    masks."""
+    shard's block count; the context option factor_split overrides), paired two items per
+    workgroup or not (factor_pair; A = 300 leaves the last pair half idle), gives the same
+    bit-exact panel and masks."""
     import torch
     import afm
     from afm.synthetic import make_panel
     p = make_panel(A, 500, seed=9, edge_cases=True, hole_frac=0.01, listing_frac=0.2)
     grid = afm.PanelGrid.from_panel(p)
-    monkeypatch.setenv("AFM_FP_TYPES", types)
-    monkeypatch.setenv("AFM_FP_PAIR", pair)
+    from afm import _lib
     fin = torch.zeros_like(grid.vbits)
-    out, nanfree = afm.factor_panel(grid, finite=fin)
+    with _lib.options(factor_split=int(types), factor_pair=int(pair)):
+        out, nanfree = afm.factor_panel(grid, finite=fin)
     torch.cuda.synchronize()
     tt, aa, ref = oracle_panel(p)
     got = out[:, torch.from_numpy(tt).cuda(), torch.from_numpy(aa).cuda()].T.cpu().numpy()
@@ -118,10 +118,11 @@ def test_clean_fast_step_matches_general_step(monkeypatch):
         p.close[int(rng.integers(100, 690)), a] = np.nan
     grid = afm.PanelGrid.from_panel(p)
     outs = {}
+    from afm import _lib
     for flag in ("1", "0"):
-        monkeypatch.setenv("AFM_FP_NOFAST", flag)
         fin = torch.zeros_like(grid.vbits)
-        out, nanfree = afm.factor_panel(grid, finite=fin)
+        with _lib.options(factor_fast=int(flag == "0")):
+            out, nanfree = afm.factor_panel(grid, finite=fin)
         torch.cuda.synchronize()
         outs[flag] = (out.clone(), nanfree.clone(), fin.clone())
     assert torch.equal(outs["1"][1], outs["0"][1]) and torch.equal(outs["1"][2], outs["0"][2])

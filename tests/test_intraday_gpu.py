@@ -85,8 +85,10 @@ def test_time_slabs_identical_to_one_launch(monkeypatch, types, step):
     import afm
     from afm.intraday import factor_panel_slabs, make_panel_device
     torch.cuda.set_device(0)
-    monkeypatch.setenv("AFM_FP_TYPES", str(types))
+    from afm import _lib
     g = make_panel_device(300, 2500, seed=9, hole_frac=0.01)
+    opts = _lib.options(factor_split=types)
+    opts.__enter__()
     full, nf_full = afm.factor_panel(g)
     vb = afm.unpack_bits(g.vbits, g.T)
     seen = []
@@ -100,5 +102,74 @@ def test_time_slabs_identical_to_one_launch(monkeypatch, types, step):
         assert torch.equal(nanfree, nf_full[w0:w1]), (t0, t1)
         seen.append((t0, t1))
 
-    n = factor_panel_slabs(g, consume, bars_per_slab=step)
+    try:
+        n = factor_panel_slabs(g, consume, bars_per_slab=step)
+    finally:
+        opts.__exit__(None, None, None)
     assert n == (g.T + step - 1) // step and seen[-1][1] == g.T
+
+
+def test_config_d_full_size_slabs_vs_oracle():
+    """BASELINE config D at full size: 3,000 assets x 196,560 one-minute bars (2 years x 252 days
+    x 390 bars, 5.6e8 present asset-bars) through the default time-slab build (factor_panel_slabs,
+    output buffer sized to the free HBM).  The consumer keeps 3 sampled assets' 98 columns and
+    nanfree bits from every slab; they are compared with the oracle's pandas-exact restatement
+    of each asset's whole series (bit-exact), and every slab's nanfree words must be a subset of
+    the presence words."""
+    import torch
+    import afm
+    import oracle
+    from afm.intraday import factor_panel_slabs, make_panel_device
+    torch.cuda.set_device(0)
+    A, T = 3000, 2 * 252 * 390
+    g = make_panel_device(A, T, seed=2024)
+    picks = [0, 1499, 2999]                            # first, middle, last (partial block) asset
+    cols = {a: [] for a in picks}
+    nfs = {a: [] for a in picks}
+    nslab = []
+
+    def consume(t0, t1, out, nanfree):
+        nw = (t1 - t0 + 63) // 64
+        assert torch.equal(nanfree & ~g.vbits[t0 // 64:t0 // 64 + nw], torch.zeros_like(nanfree))
+        for a in picks:
+            cols[a].append(out[:, :, a].cpu().numpy())                     # [98][t1 - t0]
+            nfs[a].append(afm.unpack_bits(nanfree[:, a:a + 1].contiguous(), t1 - t0)[:, 0].cpu().numpy())
+        nslab.append((t0, t1))
+
+    n = factor_panel_slabs(g, consume)
+    assert nslab[0][0] == 0 and nslab[-1][1] == T and n == len(nslab)
+    vb = afm.unpack_bits(g.vbits, T)
+    for a in picks:
+        v = vb[:, a].cpu().numpy()
+        tt = np.flatnonzero(v)
+        x = lambda t: t[:, a].cpu().numpy()[tt]                              # noqa: E731
+        ref = oracle.factors_long(np.array([0, len(tt)], np.int64), x(g.close), x(g.volume),
+                                  x(g.ret1d), x(g.excess))
+        got = np.concatenate(cols[a], axis=1)[:, tt].T
+        assert same(got, ref), (a, mismatch_report(got, ref, afm.FACTOR_NAMES))
+        nf = np.concatenate(nfs[a])
+        want = np.zeros(T, bool)
+        want[tt] = ~np.isnan(ref[:, :96]).any(axis=1)
+        assert np.array_equal(nf, want), a
+
+
+def test_slab_default_size_unaligned_series():
+    """slab_bars' default on a series that fits one slab and is not a multiple of 64 bars (the
+    round-2 advisor case): one slab, equal to one launch."""
+    import torch
+    import afm
+    from afm.intraday import factor_panel_slabs, make_panel_device, slab_bars
+    torch.cuda.set_device(0)
+    g = make_panel_device(300, 2500, seed=3, hole_frac=0.01)
+    assert slab_bars(g) % 64 == 0 and slab_bars(g) >= g.T
+    full, nf_full = afm.factor_panel(g)
+    vb = afm.unpack_bits(g.vbits, g.T)
+    got = []
+
+    def consume(t0, t1, out, nanfree):
+        m = vb[t0:t1]
+        assert torch.equal(out[:, m].nan_to_num(7.0), full[:, t0:t1][:, m].nan_to_num(7.0))
+        assert torch.equal(nanfree, nf_full)
+        got.append((t0, t1))
+
+    assert factor_panel_slabs(g, consume) == 1 and got == [(0, g.T)]

@@ -72,8 +72,9 @@ def test_gram_fast_pass_identical_to_checked(mode, monkeypatch):
         args = (flat, T * lda, 500, 500, list(range(p)), p)
         kw = dict(nseg=(T * lda + 499) // 500, row_limit=T * lda - 77)
     g1, s1 = xs_gram(*args, **kw)
-    monkeypatch.setenv("AFM_GRAM_CHECKED", "1")
-    g0, s0 = xs_gram(*args, **kw)
+    from afm import _lib
+    with _lib.options(gram_checked=1):
+        g0, s0 = xs_gram(*args, **kw)
     torch.cuda.synchronize()
     assert torch.equal(s0, s1)
     assert torch.equal(g0, g1)

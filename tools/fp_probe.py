@@ -16,12 +16,19 @@ def main():
     ap.add_argument("--assets", type=int, default=10000)
     ap.add_argument("--days", type=int, default=5040)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--listing-frac", type=float, default=0.1)
+    ap.add_argument("--fast", type=int, default=1, help="context option factor_fast")
+    ap.add_argument("--split", type=int, default=0, help="context option factor_split")
     a = ap.parse_args()
     import numpy as np
     import torch
     import afm
     from afm.synthetic import make_panel
-    grid = afm.PanelGrid.from_panel(make_panel(a.assets, a.days, seed=2023, tradable_p=0.9))
+    from afm import _lib
+    grid = afm.PanelGrid.from_panel(make_panel(a.assets, a.days, seed=2023, tradable_p=0.9,
+                                               listing_frac=a.listing_frac))
+    _lib.Context.get().set_option("factor_fast", a.fast)
+    _lib.Context.get().set_option("factor_split", a.split)
     out, nanfree = afm.factor_panel(grid)
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -38,7 +45,8 @@ def main():
     h = 0
     for v in ck:
         h = (h * 1000003 ^ v) & 0xffffffffffff
-    print(f"lib={os.environ.get('AFM_LIB') or 'default'}: factors {np.median(ts):.3f} ms "
+    print(f"lib={os.environ.get('AFM_LIB') or 'default'} A={a.assets} listing={a.listing_frac} "
+          f"fast={a.fast} split={a.split}: factors {np.median(ts):.3f} ms "
           f"(min {min(ts):.3f}); checksum {h:012x}", flush=True)
 
 
