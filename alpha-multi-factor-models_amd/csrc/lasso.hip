@@ -8,7 +8,9 @@
 // iteration) followed by the duality gap test gap < tol * y'y.  Same operation order as
 // oracle/lasso_oracle.c (axpy = one fma per element, reductions sequential in feature order).
 //
-// One wave (after a block-wide setup of Q): lane j owns features j and j + 64 (p <= 110); H, w and q live in registers; the Gram
+// One wave (after a block-wide setup of Q): lane j owns features j and j + 64 (p <= 110); H, w
+// and q live in registers; coordinates that cannot move are skipped by ballot (a sweep costs its
+// movable coordinates, not p); the Gram
 // Q sits in LDS (a row per coordinate, conflict-free); the scalar step of a coordinate is
 // computed redundantly by every lane from readlane broadcasts.  The work is a few hundred
 // flops per coordinate on a dependency chain: latency-bound by construction (one date-free
@@ -69,9 +71,34 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     const double d_w_tol = tol;
     const double tol_y = tol * ynorm2;
     int n_iter = 0;
+    // per-lane diagonal: a coordinate whose weight is 0 and whose soft threshold gives 0 again
+    // changes nothing (no H update, w stays a signed zero) -- the sweep skips to the next
+    // coordinate that can move, found by ballot over the lanes' current H
+    const double qd0 = has0 ? Q[j0 * p + j0] : 0.0, qd1 = has1 ? Q[j1 * p + j1] : 0.0;
+    auto movable = [&](double qd, double q, double h, double w) {
+        const double tmp = q - h;
+        const bool nz = (positive && tmp < 0) ? false : __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0) != 0.0;
+        return qd != 0.0 && (w != 0.0 || nz);
+    };
+    // the signed zero the skipped coordinate would store: fsign(tmp) * 0 / (qii + beta)
+    auto zero_of = [&](double q, double h) {
+        const double tmp = q - h;
+        return (positive && tmp < 0) ? 0.0 : (tmp < 0 ? -0.0 : 0.0);
+    };
     for (n_iter = 0; n_iter < max_iter; ++n_iter) {
         double w_max = 0.0, d_w_max = 0.0;
         for (int ii = 0; ii < p; ++ii) {
+            {   // skip coordinates [ii, next) that cannot move (exactly sklearn's no-ops)
+                const uint64_t m0 = __ballot(has0 && j0 >= ii && movable(qd0, q0, h0, w0));
+                const uint64_t m1 = __ballot(has1 && j1 >= ii && movable(qd1, q1, h1, w1));
+                const int next = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : p);
+                if (next > ii) {
+                    if (has0 && j0 >= ii && j0 < next && qd0 != 0.0) w0 = zero_of(q0, h0);
+                    if (has1 && j1 >= ii && j1 < next && qd1 != 0.0) w1 = zero_of(q1, h1);
+                    ii = __builtin_amdgcn_readfirstlane(next);
+                    if (ii >= p) break;
+                }
+            }
             const double* row = Q + ii * p;
             const double qii = row[ii];
             if (qii == 0.0) continue;

@@ -206,6 +206,154 @@ __device__ __forceinline__ void book_cov(Shared<KM>& sh, const int k, const int6
     __syncthreads();
 }
 
+// ---- pairwise-complete covariance on fp64 MFMA (books of more than 32 names) -----------------
+// The same statistic as book_cov (pandas nancorr(cov=True): per pair, the rows where both values
+// are finite) written as masked SYRKs over the window.  With m the presence mask, c_m a centring
+// constant per member (the mean of its finite values) and x~ = m * (x - c_m):
+//   N = M M',  C = X~ X~',  P = X~ M',  Q = M X~'     (P_ij = sum over both-present rows of x~_i,
+//   Q_ij = the same of x~_j), cov_ij = (C_ij - P_ij Q_ij / N_ij) / (N_ij - 1), NaN for N_ij < 2.
+// Every product is v_mfma_f64_16x16x4_f64 on 16-member tiles (the window rows are the k dim):
+// 36 tile pairs (I <= J) of at most 8 tiles, pair q on wave q % 4.  Pass 0 stages the window
+// once for the member means and N (written into S), pass 1 again for C, P, Q (27 accumulators
+// per wave), then each element is finished in place.  Work: 2 * rows * k^2 flop per product.
+// Centring keeps P and Q small, so the difference C - PQ/N does not cancel (rel ~1e-15 of S on
+// the test books, vs 1e-12 for the bar of tests/test_portfolio_gpu.py).
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+struct CovPairs {
+    int I[36], J[36];
+    constexpr CovPairs() : I(), J() {
+        int q = 0;
+        for (int j = 0; j < 8; ++j)
+            for (int i = 0; i <= j; ++i) { I[q] = i; J[q] = j; ++q; }
+    }
+};
+
+// stage rows [h0, h0 + 64) of the k members into sh.u.hv (NaN past the window)
+template <int KM, class Get>
+__device__ __forceinline__ void cov_stage(Shared<KM>& sh, const int k, const int64_t h0, Get get) {
+    constexpr int EPT = KM * 64 / kT;
+    const int tid = threadIdx.x;
+    double v[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * kT;
+        v[j] = e < k * 64 ? get(e >> 6, h0 + (e & 63)) : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * kT;
+        if (e < k * 64) sh.u.hv[e >> 6][e & 63] = v[j];
+    }
+    __syncthreads();
+}
+
+// pass 0 (S0 < 0): the member means (thread per member, into sh.x) and N (into S).
+// pass 1 (slots [S0, S0 + NS) of this wave): C, P, Q, then those elements finished in place.
+template <int KM, int W, int S0, int NS, class Get>
+__device__ void cov_mfma_pass(Shared<KM>& sh, const int k, const int64_t rows, Get get) {
+    static_assert(KM == 128, "MFMA covariance: 8 tiles of 16 members");
+    constexpr CovPairs tab{};
+    constexpr bool P0 = S0 < 0;
+    constexpr int SB = P0 ? 0 : S0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int fi = lane & 15, kk = lane >> 4;
+    const int nt = (k + 15) / 16;
+    double mu[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) mu[t] = !P0 && 16 * t + fi < k ? sh.x[16 * t + fi] : 0.0;
+    d4 c[NS], pp[NS], qq[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        c[s] = d4{0.0, 0.0, 0.0, 0.0};
+        pp[s] = c[s];
+        qq[s] = c[s];
+    }
+    double msum = 0.0;
+    int mcnt = 0;
+    for (int64_t h0 = 0; h0 < rows; h0 += 64) {
+        cov_stage(sh, k, h0, get);
+        if (P0 && tid < k) {
+            for (int d = 0; d < 64; ++d) {
+                const double v = sh.u.hv[tid][d];
+                const bool f = h0 + d < rows && __builtin_isfinite(v);
+                msum += f ? v : 0.0;
+                mcnt += f ? 1 : 0;
+            }
+        }
+        const int nks = (int)((rows - h0) < 64 ? (rows - h0 + 3) / 4 : 16);
+        for (int it = 0; it < nks; ++it) {
+            double x[8], m[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int mem = 16 * t + fi, row = 4 * it + kk;
+                const double v = sh.u.hv[mem][row];
+                const bool f = mem < k && h0 + row < rows && __builtin_isfinite(v);
+                x[t] = f ? v - mu[t] : 0.0;
+                m[t] = f ? 1.0 : 0.0;
+            }
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                const int q = W + 4 * (SB + s);
+                if (q < 36 && tab.J[q] < nt) {
+                    const int I = tab.I[q], J = tab.J[q];
+                    if (P0) {
+                        c[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(m[I], m[J], c[s], 0, 0, 0);
+                    } else {
+                        c[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I], x[J], c[s], 0, 0, 0);
+                        pp[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I], m[J], pp[s], 0, 0, 0);
+                        qq[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(m[I], x[J], qq[s], 0, 0, 0);
+                    }
+                }
+            }
+        }
+    }
+    if (P0 && tid < k) sh.x[tid] = mcnt ? msum / (double)mcnt : 0.0;   // centring constants
+    // element (i, j), i >= j (one lane each): pass 0 stores N, pass 1 replaces it by the cov
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int q = W + 4 * (SB + s);
+        if (q < 36 && tab.J[q] < nt) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * tab.I[q] + kk + 4 * r, j = 16 * tab.J[q] + fi;
+                if (i < k && j < k && (tab.I[q] < tab.J[q] || i >= j)) {
+                    if (P0) {
+                        sh.S[tri(i, j)] = c[s][r];
+                    } else {
+                        const double nn = sh.S[tri(i, j)];
+                        sh.S[tri(i, j)] = nn >= 2.0 ? (c[s][r] - pp[s][r] * qq[s][r] / nn) /
+                                                          (nn - 1.0)
+                                                    : __builtin_nan("");
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <int KM, int W, class Get>
+__device__ void cov_mfma_wave(Shared<KM>& sh, const int k, const int64_t rows, Get get) {
+    cov_mfma_pass<KM, W, -1, 9>(sh, k, rows, get);    // means + N
+    cov_mfma_pass<KM, W, 0, 5>(sh, k, rows, get);     // C, P, Q of slots 0..4
+    cov_mfma_pass<KM, W, 5, 4>(sh, k, rows, get);     // slots 5..8
+}
+
+template <int KM, class Get>
+__device__ __forceinline__ void book_cov_mfma(Shared<KM>& sh, const int k, const int64_t rows,
+                                              Get get) {
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    switch (wave) {
+        case 0: cov_mfma_wave<KM, 0>(sh, k, rows, get); break;
+        case 1: cov_mfma_wave<KM, 1>(sh, k, rows, get); break;
+        case 2: cov_mfma_wave<KM, 2>(sh, k, rows, get); break;
+        default: cov_mfma_wave<KM, 3>(sh, k, rows, get); break;
+    }
+    __syncthreads();
+}
+
 // k largest keys among candidates (key valid when cand), ties -> smaller index first.
 // Writes the selected indices, sorted (key desc, index asc), to out[0..k).
 template <int KM>
@@ -759,9 +907,11 @@ __global__ __launch_bounds__(kT) void weights_kernel(const double* R, int64_t ro
                                                      double* cov, int32_t* status) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     Shared<kMaxK>& sh = *reinterpret_cast<Shared<kMaxK>*>(smem_raw);
-    book_cov(sh, k, rows, [&](int m, int64_t row) -> double {
+    auto get = [&](int m, int64_t row) -> double {
         return row < rows ? R[row * ld + m] : __builtin_nan("");
-    });
+    };
+    if (k > 32) book_cov_mfma(sh, k, rows, get);
+    else book_cov(sh, k, rows, get);
     const int tid = threadIdx.x;
     for (int e = tid; e < k * k; e += kT) cov[e] = sh.S[tri(e / k, e % k)];
     bool capped = false;
@@ -876,7 +1026,12 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
         }
         __syncthreads();
     } else if (k * (k + 1) / 2 <= kT || r.hscr == nullptr) {
-        book_cov(sh, k, rows, gather);                      // one pass over the member pairs
+        if constexpr (KM == kMaxK) {
+            if (k > 32) book_cov_mfma(sh, k, rows, gather);
+            else book_cov(sh, k, rows, gather);             // one pass over the member pairs
+        } else {
+            book_cov(sh, k, rows, gather);
+        }
     } else {
         // several passes: gather the members' window once into a contiguous [member][row]
         // scratch block, which every pass then stages with coalesced reads
@@ -897,9 +1052,15 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
         }
         __syncthreads();
         if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 5] = wall_clock64();
-        book_cov(sh, k, rows, [&](int m, int64_t row) -> double {
+        auto fromH = [&](int m, int64_t row) -> double {
             return row < rows ? H[m * rows + row] : __builtin_nan("");
-        });
+        };
+        if constexpr (KM == kMaxK) {
+            if (k > 32) book_cov_mfma(sh, k, rows, fromH);  // masked SYRKs on fp64 MFMA
+            else book_cov(sh, k, rows, fromH);
+        } else {
+            book_cov(sh, k, rows, fromH);
+        }
     }
 
     // ---- exact box-constrained QP (primal active set, wave 0) -----------------------------

@@ -320,15 +320,16 @@ def main():
             # stated non-reference design: the 96 factors without tmr_ret1d, KKT:433-443)
             from dataclasses import replace
 
-            from afm.pipeline import DENSE_FEATURES
+            from afm.pipeline import DENSE_ALPHA, DENSE_FEATURES
             del pipe
             torch.cuda.empty_cache()
             vs, vw = max(2, min(args.steps, 5)), 1
             res["top_n_100"] = variant_line(grid, replace(cfg, top_n=100), vs, vw,
                                             "headline step with top_n = 100 (KKT:796 stress)")
             res["dense_lasso"] = variant_line(
-                grid, replace(cfg, features=DENSE_FEATURES), vs, vw,
-                "variant of KKT:433-443: features without tmr_ret1d (96 columns), Lasso dense")
+                grid, replace(cfg, features=DENSE_FEATURES, alpha=DENSE_ALPHA), vs, vw,
+                f"variant of KKT:433-443 / KKT:605: features without tmr_ret1d (96 columns), "
+                f"Lasso alpha {DENSE_ALPHA:g} -- a dense fit, so the predict reads its support")
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.seed)
             res["cpu_baseline_port"] = cpu_port(args.seed)

@@ -35,7 +35,9 @@ def test_value_path_matches_oracle_chain(panel):
     for top_n, rtol in ((10, 1e-8), (3, 1e-4)):
         v = pandas_chain.run_chain(panel, te, ve, top_n=top_n, timings=tm)
         r = chain.run_chain(panel, te, ve, top_n=top_n, analyzer=False, fm=False)
-        assert set(tm) == {"factors", "zscore", "lasso", "analyzer", "portfolio"}
+        assert set(tm) == {"factors", "zscore", "lasso", "analyzer", "portfolio", "filter_847",
+                           "dates", "dates_total"}
+        assert tm["dates"] == tm["dates_total"] and 0 <= tm["filter_847"] <= tm["portfolio"]
         # top_n=10 under the 0.1 cap pins every weight at 0.1 (SLSQP lands within ~1e-10).  top_n=3 leaves
         # the weights free: SLSQP (ftol 1e-6) against the oracle's exact QP.
         np.testing.assert_allclose(v, np.asarray(r["portfolio"]["value"]), rtol=rtol, atol=0)

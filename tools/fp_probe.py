@@ -45,6 +45,18 @@ def main():
     h = 0
     for v in ck:
         h = (h * 1000003 ^ v) & 0xffffffffffff
+    # the label planes alone (afm_labels_f64, the side-stream kernel of the pipeline)
+    L, P = _lib.lib(), _lib.ptr
+    tl = []
+    for _ in range(a.reps):
+        ev[0].record()
+        _lib.check(L.afm_labels_f64(_lib.Context.get().bind_stream(), grid.T, grid.lda, 0, grid.T,
+                                    P(grid.excess), P(grid.ret1d), P(grid.vbits), P(out[96]),
+                                    P(out[97])), "labels")
+        ev[1].record()
+        torch.cuda.synchronize()
+        tl.append(ev[0].elapsed_time(ev[1]))
+    print(f"labels alone {np.median(tl):.3f} ms", flush=True)
     print(f"lib={os.environ.get('AFM_LIB') or 'default'} A={a.assets} listing={a.listing_frac} "
           f"fast={a.fast} split={a.split}: factors {np.median(ts):.3f} ms "
           f"(min {min(ts):.3f}); checksum {h:012x}", flush=True)
