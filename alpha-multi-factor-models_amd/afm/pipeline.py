@@ -100,11 +100,13 @@ class PipelineConfig:
     # variant may name another subset -- e.g. DENSE_FEATURES, which drops tmr_ret1d (the
     # undemeaned twin of the target, NT:90-91) so the Lasso keeps many coefficients
     features: tuple | None = None
-    # one GPU: the per-date FM Grams run right after the factor kernel, beside the z-score
+    # True (one GPU): the per-date FM Grams run right after the factor kernel, beside the z-score
     # statistics, over the factor rows (frows); once the z-score rows exist, only the blocks that
     # hold a dropped asset are recomputed (afm_zgram_select_f64) -- the same partials as one pass
-    # over the z-score rows.  False: one pass after the predict (round-2 placement).
-    fm_early: bool = True
+    # over the z-score rows.  Measured slower (46.2 vs 35.5 ms/step at config C: the FM MFMA
+    # Grams then share the SIMDs with the z statistics and the pooled Gram, 12.0 -> 19.6 ms), so
+    # the default is one pass after the predict.
+    fm_early: bool = False
 
 
 @dataclass

@@ -30,9 +30,9 @@
 //    correctly rounded reciprocal table and one Markstein correction -- the exactly rounded
 //    quotient for every integer divisor <= 64 (FMA; no contraction elsewhere); ewm skips its
 //    division by (old + alpha) == 1.0 exactly.  Other divisions are IEEE.
-//  * dropna bookkeeping: each wave ORs its per-lane "some output NaN / non-finite at day s" bits
-//    into LDS words; at each 64-day word the workgroup stores its type's partial masks, and
-//    masks_kernel combines the kTypes partials into nanfree / finite.
+//  * dropna bookkeeping: each job wave keeps its per-lane "some output NaN / non-finite at day s"
+//    bits and stores them at each 64-day word; masks_kernel ORs the kJobSets partials into
+//    nanfree / finite.
 //
 // Algorithmic traffic per present asset-day: 32 B of inputs read + 98 x 8 B written = 816 B.
 #include "afm_internal.h"
@@ -49,7 +49,14 @@ constexpr int kChunk = 8;
 // the loader fills chunk c+1 while the job waves scan chunk c: the ring must hold the scan's
 // lookback (57) plus two chunks
 constexpr int kRing = 57 + 2 * kChunk + 1;
-constexpr int kJobSets = 15;      // job waves per 64-asset block (W0..W14 below)
+// job waves per 64-asset block (the partition W0.. below): 15 job sets, three items of 5 job
+// waves + a loader, two items per workgroup = 3 waves per SIMD at <= 168 VGPRs; or 21 job sets,
+// three items of 7 + a loader, 4 waves per SIMD at <= 128 VGPRs
+#ifndef AFM_FP_SETS
+#define AFM_FP_SETS 15
+#endif
+constexpr int kJobSets = AFM_FP_SETS;
+static_assert(kJobSets == 15 || kJobSets == 21, "job-set partitions: 15 or 21");
 
 typedef unsigned long long u64;
 #ifdef AFM_FP_PROFILE
@@ -77,8 +84,6 @@ struct Smem {
     double rtab[128];          // rtab[n] = 1.0 / n (IEEE), rtab[0] = +inf; indexed n & 127
     int cbyte[2][kLanes];      // presence bits of chunk c (parity c & 1), written by the loader
     int okbyte[2][kLanes];     // chunk c: 2 every present day clean (kClean), 1 warm, 0 general
-    u64 nanmask[kLanes];
-    u64 badmask[kLanes];       // some factor non-finite (NaN or +-inf)
 };
 
 // ---- clean windows ----------------------------------------------------------------------------
@@ -120,8 +125,8 @@ struct Args {
     const GLB double* volume;
     const GLB uint64_t* vbits;
     GLB double* out;
-    GLB uint64_t* nanpart;     // [types][nch][lda] per-workgroup-type "some output NaN" bits
-    GLB uint64_t* badpart;     // [types][nch][lda] per-type "some output non-finite" bits
+    GLB uint64_t* nanpart;     // [kJobSets][words][lda] per-job-wave "some output NaN" bits
+    GLB uint64_t* badpart;     // [kJobSets][words][lda] per-job-wave "some output non-finite" bits
     int types;                 // workgroups per 64-asset block (1, 3, 5 or 15)
     int fast;                  // 0: general step only (A/B tests)
     int nblk;                  // 64-asset blocks (paired launch: items = nblk * types)
@@ -211,6 +216,48 @@ struct Step {
     __device__ __forceinline__ double fret(int L) const { return L == 0 ? r0 : C(L) / C(L + 1) - 1; }
     __device__ __forceinline__ double fvolchg(int L) const { return L == 0 ? g0 : V(L) / V(L + 1) - 1; }
 };
+
+// A clean or warm step's view (see kClean): every ring value the wave's jobs read, gathered at the
+// top of the step in one batch of LDS reads (CM / VM: bit L = lookback L of close / volume), so
+// the step waits for LDS once instead of once per job.  A job reads a lookback its pack did not
+// gather only by a compile error.
+constexpr int kLook = 58;            // lookbacks 0 .. 57 (ACCEL_56 reads close 57 back)
+// s_waitcnt vmcnt(0) with expcnt / lgkmcnt left at their maxima (gfx9 encoding)
+constexpr int kWaitVm0 = 0x0f70;
+template <u64 CM, u64 VM>
+struct FastStep : Step {
+    double cc[kLook], vc[kLook];
+    __device__ __forceinline__ void gather() {
+#pragma unroll
+        for (int L = 0; L < kLook; ++L) {
+            if ((CM >> L) & 1ull) cc[L] = C(L);
+            if ((VM >> L) & 1ull) vc[L] = V(L);
+        }
+    }
+    template <int L>
+    __device__ __forceinline__ double c() const {
+        static_assert(L < kLook && ((CM >> L) & 1ull), "close lookback not gathered");
+        return cc[L];
+    }
+    template <int L>
+    __device__ __forceinline__ double v() const {
+        static_assert(L < kLook && ((VM >> L) & 1ull), "volume lookback not gathered");
+        return vc[L];
+    }
+    template <int L>
+    __device__ __forceinline__ double fret() const {
+        if constexpr (L == 0) return r0;
+        else return c<L>() / c<L + 1>() - 1;
+    }
+    template <int L>
+    __device__ __forceinline__ double fvolchg() const {
+        if constexpr (L == 0) return g0;
+        else return v<L>() / v<L + 1>() - 1;
+    }
+};
+constexpr u64 lb(int L) { return 1ull << L; }
+#define FC(L) s.template c<(L)>()
+#define FV(L) s.template v<(L)>()
 
 // ---- pandas window kernels as register-resident recurrences -------------------------------
 // roll_mean (pandas/_libs/window/aggregations.pyx): Kahan add/remove with separate
@@ -419,6 +466,7 @@ struct ComC {
 // step(): any day (pandas semantics in full); fstep(): a clean day (see kClean).
 template <int W>
 struct Sma {  // No-talib.py:9-10
+    static constexpr u64 kC = lb(0) | lb(W), kV = 0;
     RollMean m;
     __device__ void init() { m.init(); }
     __device__ void step(Step& s) {
@@ -426,13 +474,13 @@ struct Sma {  // No-talib.py:9-10
         m.add(s.C(0));
         s.put((W - 6) / 4, m.result(s, W, s.rn->C));
     }
-    __device__ void fstep(Step& s) {
-        m.fremove(s.C(W));
-        m.fadd(s.C(0));
+    template <class S> __device__ void fstep(S& s) {
+        m.fremove(FC(W));
+        m.fadd(FC(0));
         s.putf((W - 6) / 4, m.fresult_pos<W>(s.rn->C));
     }
-    __device__ void wstep(Step& s) {
-        m.wstep(s.p >= W ? s.C(W) : 0.0, s.C(0), s.p >= W ? W : s.p + 1);
+    template <class S> __device__ void wstep(S& s) {
+        m.wstep(s.p >= W ? FC(W) : 0.0, FC(0), s.p >= W ? W : s.p + 1);
         const double r = m.fresult_pos<W>(s.rn->C);
         s.putf((W - 6) / 4, s.p >= W - 1 ? r : qnan());
     }
@@ -440,21 +488,23 @@ struct Sma {  // No-talib.py:9-10
 
 template <int W>
 struct Ema {  // No-talib.py:13-14
+    static constexpr u64 kC = lb(0), kV = 0;
     Ewm e;
     __device__ void init() { e.init(); }
     __device__ void step(Step& s) {
         s.put(12 + (W - 6) / 4, e.step(s.C(0), SpanC<W>::owf, SpanC<W>::alpha));
     }
-    __device__ void fstep(Step& s) {
-        s.putf(12 + (W - 6) / 4, e.fstep(s.C(0), SpanC<W>::owf, SpanC<W>::alpha));
+    template <class S> __device__ void fstep(S& s) {
+        s.putf(12 + (W - 6) / 4, e.fstep(FC(0), SpanC<W>::owf, SpanC<W>::alpha));
     }
-    __device__ void wstep(Step& s) {
-        s.putf(12 + (W - 6) / 4, e.wstep(s.C(0), SpanC<W>::owf, SpanC<W>::alpha, s.p, 0));
+    template <class S> __device__ void wstep(S& s) {
+        s.putf(12 + (W - 6) / 4, e.wstep(FC(0), SpanC<W>::owf, SpanC<W>::alpha, s.p, 0));
     }
 };
 
 template <int W>
 struct Vwma {  // No-talib.py:17-19
+    static constexpr u64 kC = lb(0) | lb(W), kV = lb(0) | lb(W);
     RollMean mvc, mv;
     __device__ void init() { mvc.init(); mv.init(); }
     __device__ void step(Step& s) {
@@ -468,21 +518,21 @@ struct Vwma {  // No-talib.py:17-19
         mv.add(v0);
         s.put(24 + (W - 6) / 4, mvc.result(s, W, s.rn->VC) / mv.result(s, W, s.rn->V));
     }
-    __device__ void fstep(Step& s) {
-        const double vq = s.V(W);
-        mvc.fremove(vq * s.C(W));
+    template <class S> __device__ void fstep(S& s) {
+        const double vq = FV(W);
+        mvc.fremove(vq * FC(W));
         mv.fremove(vq);
-        mvc.fadd(s.V(0) * s.C(0));
-        mv.fadd(s.V(0));
+        mvc.fadd(FV(0) * FC(0));
+        mv.fadd(FV(0));
         // a volume mean can round to 0 -> track
         s.put(24 + (W - 6) / 4, mvc.fresult_pos<W>(s.rn->VC) / mv.fresult_pos<W>(s.rn->V));
     }
-    __device__ void wstep(Step& s) {
+    template <class S> __device__ void wstep(S& s) {
         const bool rm = s.p >= W;
         const int n = rm ? W : s.p + 1;
-        const double vq = rm ? s.V(W) : 0.0, cq = rm ? s.C(W) : 0.0;
-        const double v0 = s.V(0);
-        mvc.wstep(vq * cq, v0 * s.C(0), n);
+        const double vq = rm ? FV(W) : 0.0, cq = rm ? FC(W) : 0.0;
+        const double v0 = FV(0);
+        mvc.wstep(vq * cq, v0 * FC(0), n);
         mv.wstep(vq, v0, n);
         const double r = mvc.fresult_pos<W>(s.rn->VC) / mv.fresult_pos<W>(s.rn->V);
         s.put(24 + (W - 6) / 4, s.p >= W - 1 ? r : qnan());
@@ -491,6 +541,7 @@ struct Vwma {  // No-talib.py:17-19
 
 template <int W>
 struct Bbands {  // No-talib.py:22-26
+    static constexpr u64 kC = lb(0) | lb(W), kV = 0;
     RollMean m;
     RollVar v;
     __device__ void init() { m.init(); v.init(); }
@@ -508,8 +559,8 @@ struct Bbands {  // No-talib.py:22-26
         s.put(col, ma + (2 * sd));
         s.put(col + 1, ma - (2 * sd));
     }
-    __device__ void fstep(Step& s) {
-        const double xr = s.C(W), x = s.C(0);
+    template <class S> __device__ void fstep(S& s) {
+        const double xr = FC(W), x = FC(0);
         m.fremove(xr);
         v.fremove<W>(xr);
         m.fadd(x);
@@ -519,11 +570,11 @@ struct Bbands {  // No-talib.py:22-26
         s.putf(col, ma + (2 * sd));
         s.putf(col + 1, ma - (2 * sd));
     }
-    __device__ void wstep(Step& s) {
+    template <class S> __device__ void wstep(S& s) {
         const bool rm = s.p >= W;
-        const double x = s.C(0);
-        m.wstep(rm ? s.C(W) : 0.0, x, rm ? W : s.p + 1);
-        if (rm) v.fremove<W>(s.C(W));
+        const double x = FC(0);
+        m.wstep(rm ? FC(W) : 0.0, x, rm ? W : s.p + 1);
+        if (rm) v.fremove<W>(FC(W));
         v.wadd(s, x, rm ? W : s.p + 1);
         const double ma = m.fresult_pos<W>(s.rn->C), sd = zsqrt(v.fresult<W>(s.rn->C));
         const bool full = s.p >= W - 1;
@@ -535,6 +586,7 @@ struct Bbands {  // No-talib.py:22-26
 
 template <int W>
 struct MomAccelRocr {  // No-talib.py:35-44
+    static constexpr u64 kC = lb(0) | lb(1) | lb(W) | lb(W + 1), kV = 0;
     __device__ void init() {}
     __device__ void step(Step& s) {
         const int k = (W - 14) / 6;
@@ -549,26 +601,27 @@ struct MomAccelRocr {  // No-talib.py:35-44
         s.put(60 + k, acc);
         s.put(68 + k, roc);
     }
-    __device__ void fstep(Step& s) {
+    template <class S> __device__ void fstep(S& s) {
         const int k = (W - 14) / 6;
-        const double c = s.C(0), cw = s.C(W);
+        const double c = FC(0), cw = FC(W);
         const double mom = c - cw;
         s.putf(52 + k, mom);
-        s.putf(60 + k, mom - (s.C(1) - s.C(1 + W)));
+        s.putf(60 + k, mom - (FC(1) - FC(1 + W)));
         s.putf(68 + k, c / cw - 1);
     }
-    __device__ void wstep(Step& s) {
+    template <class S> __device__ void wstep(S& s) {
         const int k = (W - 14) / 6;
-        const double c = s.C(0), cw = s.C(W);
+        const double c = FC(0), cw = FC(W);
         const double mom = c - cw;
         s.putf(52 + k, s.p >= W ? mom : qnan());
-        s.putf(60 + k, s.p >= W + 1 ? mom - (s.C(1) - s.C(1 + W)) : qnan());
+        s.putf(60 + k, s.p >= W + 1 ? mom - (FC(1) - FC(1 + W)) : qnan());
         s.putf(68 + k, s.p >= W ? c / cw - 1 : qnan());
     }
 };
 
 template <int SLOW>
 struct Macd {  // No-talib.py:47-50
+    static constexpr u64 kC = lb(0), kV = 0;
     Ewm fast, slow;
     __device__ void init() { fast.init(); slow.init(); }
     __device__ void step(Step& s) {
@@ -577,14 +630,14 @@ struct Macd {  // No-talib.py:47-50
         double l = slow.step(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha);
         s.put(76 + (SLOW - 18) / 6, f - l);
     }
-    __device__ void fstep(Step& s) {
-        const double c = s.C(0);
+    template <class S> __device__ void fstep(S& s) {
+        const double c = FC(0);
         const double f = fast.fstep(c, SpanC<12>::owf, SpanC<12>::alpha);
         const double l = slow.fstep(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha);
         s.putf(76 + (SLOW - 18) / 6, f - l);
     }
-    __device__ void wstep(Step& s) {
-        const double c = s.C(0);
+    template <class S> __device__ void wstep(S& s) {
+        const double c = FC(0);
         const double f = fast.wstep(c, SpanC<12>::owf, SpanC<12>::alpha, s.p, 0);
         const double l = slow.wstep(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha, s.p, 0);
         s.putf(76 + (SLOW - 18) / 6, f - l);
@@ -593,6 +646,7 @@ struct Macd {  // No-talib.py:47-50
 
 template <int I>
 struct Rsi {  // No-talib.py:53-59
+    static constexpr u64 kC = lb(0) | lb(1), kV = 0;
     Ewm up, dn;
     __device__ void init() { up.init(); dn.init(); }
     __device__ void step(Step& s) {
@@ -605,8 +659,8 @@ struct Rsi {  // No-talib.py:53-59
         double rs = eu / ed;
         s.put(79 + (I - 8) / 6, 100 - (100 / (1 + rs)));
     }
-    __device__ void fstep(Step& s) {
-        const double d = s.C(0) - s.C(1);
+    template <class S> __device__ void fstep(S& s) {
+        const double d = FC(0) - FC(1);
         const double u = d >= 0 ? d : 0.0;
         const double w = -(d <= 0 ? d : 0.0);
         const double eu = up.fstep(u, ComC<I - 1>::owf, ComC<I - 1>::alpha);
@@ -615,8 +669,8 @@ struct Rsi {  // No-talib.py:53-59
         s.put(79 + (I - 8) / 6, 100 - (100 / (1 + rs)));     // 0 / 0 on flat prices -> track
     }
     // the up / down moves are observed from p = 1 (day 0's diff is NaN: both ewms stay NaN)
-    __device__ void wstep(Step& s) {
-        const double d = s.C(0) - s.C(1);
+    template <class S> __device__ void wstep(S& s) {
+        const double d = FC(0) - FC(1);
         const double u = d >= 0 ? d : 0.0;
         const double w = -(d <= 0 ? d : 0.0);
         const double eu = up.wstep(u, ComC<I - 1>::owf, ComC<I - 1>::alpha, s.p, 1);
@@ -627,6 +681,7 @@ struct Rsi {  // No-talib.py:53-59
 };
 
 struct PvtObvPsy {  // No-talib.py:62-69
+    static constexpr u64 kC = lb(0) | lb(1) | lb(14) | lb(15), kV = lb(0);
     double pvt, obv;
     int ups;
     __device__ void init() { pvt = 0.0; obv = 0.0; ups = 0; }
@@ -647,30 +702,31 @@ struct PvtObvPsy {  // No-talib.py:62-69
         ups -= (p >= 15 && s.C(14) > s.C(15)) ? 1 : 0;
         s.put(84, p >= 13 ? s.div((double)ups, 14) * 100 : qnan());
     }
-    __device__ void fstep(Step& s) {
-        const double c = s.C(0), v = s.V(0), c1 = s.C(1);
+    template <class S> __device__ void fstep(S& s) {
+        const double c = FC(0), v = FV(0), c1 = FC(1);
         pvt = pvt + v * (c / c1 - 1);
         s.put(82, pvt);                                   // an earlier inf term persists -> track
         obv = obv + v * ((c - c1 <= 0) ? -1.0 : 1.0);
         s.put(83, obv);
-        ups += (c > c1 ? 1 : 0) - (s.C(14) > s.C(15) ? 1 : 0);
+        ups += (c > c1 ? 1 : 0) - (FC(14) > FC(15) ? 1 : 0);
         s.putf(84, divc<14>((double)ups) * 100);
     }
-    __device__ void wstep(Step& s) {
+    template <class S> __device__ void wstep(S& s) {
         const int p = s.p;
-        const double c = s.C(0), v = s.V(0), c1 = s.C(1);
+        const double c = FC(0), v = FV(0), c1 = FC(1);
         const double pv = pvt + v * (c / c1 - 1);
         pvt = p >= 1 ? pv : pvt;
         s.put(82, p >= 1 ? pvt : qnan());
         obv = obv + v * ((p >= 1 && c - c1 <= 0) ? -1.0 : 1.0);   // day 0: NaN diff -> +volume
         s.put(83, obv);
-        ups += (p >= 1 && c > c1 ? 1 : 0) - (p >= 15 && s.C(14) > s.C(15) ? 1 : 0);
+        ups += (p >= 1 && c > c1 ? 1 : 0) - (p >= 15 && FC(14) > FC(15) ? 1 : 0);
         s.putf(84, p >= 13 ? divc<14>((double)ups) * 100 : qnan());
     }
 };
 
 template <int W, int COL>
 struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
+    static constexpr u64 kC = lb(W) | lb(W + 1), kV = 0;
     RollVar v;
     __device__ void init() { v.init(); }
     __device__ double step(Step& s) {
@@ -680,16 +736,16 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
         s.put(COL, r);
         return r;
     }
-    __device__ double fstep(Step& s) {
-        v.fremove<W>(s.fret(W));
+    template <class S> __device__ double fstep(S& s) {
+        v.fremove<W>(s.template fret<W>());
         v.fadd<W>(s.r0);
         const double r = zsqrt(v.fresult<W>(s.rn->R));
         s.putf(COL, r);
         return r;
     }
     // returns start at p = 1: the window holds min(p, W) of them, the first remove is at W + 1
-    __device__ double wstep(Step& s) {
-        if (s.p >= W + 1) v.fremove<W>(s.fret(W));
+    template <class S> __device__ double wstep(S& s) {
+        if (s.p >= W + 1) v.fremove<W>(s.template fret<W>());
         if (s.p >= 1) v.wadd(s, s.r0, s.p >= W ? W : s.p);
         const double r = s.p >= W ? zsqrt(v.fresult<W>(s.rn->R)) : qnan();
         s.putf(COL, r);
@@ -699,25 +755,27 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
 
 struct RetSd3 {
     RetSd<3, 85> a;
+    static constexpr u64 kC = RetSd<3, 85>::kC, kV = 0;
     __device__ void init() { a.init(); }
     __device__ void step(Step& s) { a.step(s); }
-    __device__ void fstep(Step& s) { a.fstep(s); }
-    __device__ void wstep(Step& s) { a.wstep(s); }
+    template <class S> __device__ void fstep(S& s) { a.fstep(s); }
+    template <class S> __device__ void wstep(S& s) { a.wstep(s); }
 };
 
 struct RetSd5x15 {  // sd_5, sd_15, sd5_15
     RetSd<5, 86> a;
     RetSd<15, 87> b;
+    static constexpr u64 kC = RetSd<5, 86>::kC | RetSd<15, 87>::kC, kV = 0;
     __device__ void init() { a.init(); b.init(); }
     __device__ void step(Step& s) {
         double x = a.step(s), y = b.step(s);
         s.put(88, x / y);
     }
-    __device__ void fstep(Step& s) {
+    template <class S> __device__ void fstep(S& s) {
         double x = a.fstep(s), y = b.fstep(s);
         s.put(88, x / y);
     }
-    __device__ void wstep(Step& s) {
+    template <class S> __device__ void wstep(S& s) {
         double x = a.wstep(s), y = b.wstep(s);
         s.put(88, x / y);
     }
@@ -725,6 +783,7 @@ struct RetSd5x15 {  // sd_5, sd_15, sd5_15
 
 template <int W, int COL>
 struct VolSd {  // volsd_W (No-talib.py:79-80)
+    static constexpr u64 kC = 0, kV = lb(0) | lb(W);
     RollVar v;
     __device__ void init() { v.init(); }
     __device__ double step(Step& s) {
@@ -734,16 +793,16 @@ struct VolSd {  // volsd_W (No-talib.py:79-80)
         s.put(COL, r);
         return r;
     }
-    __device__ double fstep(Step& s) {
-        v.fremove<W>(s.V(W));
-        v.fadd<W>(s.V(0));
+    template <class S> __device__ double fstep(S& s) {
+        v.fremove<W>(FV(W));
+        v.fadd<W>(FV(0));
         const double r = zsqrt(v.fresult<W>(s.rn->VP));
         s.putf(COL, r);
         return r;
     }
-    __device__ double wstep(Step& s) {
-        if (s.p >= W) v.fremove<W>(s.V(W));
-        v.wadd(s, s.V(0), s.p >= W ? W : s.p + 1);
+    template <class S> __device__ double wstep(S& s) {
+        if (s.p >= W) v.fremove<W>(FV(W));
+        v.wadd(s, FV(0), s.p >= W ? W : s.p + 1);
         const double r = s.p >= W - 1 ? zsqrt(v.fresult<W>(s.rn->VP)) : qnan();
         s.putf(COL, r);
         return r;
@@ -752,25 +811,27 @@ struct VolSd {  // volsd_W (No-talib.py:79-80)
 
 struct VolSd3 {
     VolSd<3, 89> a;
+    static constexpr u64 kC = 0, kV = VolSd<3, 89>::kV;
     __device__ void init() { a.init(); }
     __device__ void step(Step& s) { a.step(s); }
-    __device__ void fstep(Step& s) { a.fstep(s); }
-    __device__ void wstep(Step& s) { a.wstep(s); }
+    template <class S> __device__ void fstep(S& s) { a.fstep(s); }
+    template <class S> __device__ void wstep(S& s) { a.wstep(s); }
 };
 
 struct VolSd5x15 {
     VolSd<5, 90> a;
     VolSd<15, 91> b;
+    static constexpr u64 kC = 0, kV = VolSd<5, 90>::kV | VolSd<15, 91>::kV;
     __device__ void init() { a.init(); b.init(); }
     __device__ void step(Step& s) {
         double x = a.step(s), y = b.step(s);
         s.put(92, x / y);
     }
-    __device__ void fstep(Step& s) {
+    template <class S> __device__ void fstep(S& s) {
         double x = a.fstep(s), y = b.fstep(s);
         s.put(92, x / y);
     }
-    __device__ void wstep(Step& s) {
+    template <class S> __device__ void wstep(S& s) {
         double x = a.wstep(s), y = b.wstep(s);
         s.put(92, x / y);
     }
@@ -780,6 +841,7 @@ struct VolSd5x15 {
 // inputs).  WITH_VC also emits the vol_change column.
 template <int W, bool WITH_VC>
 struct Corr {
+    static constexpr u64 kC = lb(W) | lb(W + 1), kV = lb(W) | lb(W + 1);
     RollMean mxy, mx, my;
     RollVar vx, vy;
     int cnt;
@@ -820,8 +882,8 @@ struct Corr {
         if (WITH_VC) s.put(93, s.volchg(0));
     }
     // clean: X = ret, Y = vol_change (finite), cnt = W; c / (c - 1) is the constant W / (W - 1)
-    __device__ void fstep(Step& s) {
-        const double Xr = s.fret(W), Yr = s.fvolchg(W), X = s.r0, Y = s.g0;
+    template <class S> __device__ void fstep(S& s) {
+        const double Xr = s.template fret<W>(), Yr = s.template fvolchg<W>(), X = s.r0, Y = s.g0;
         const double XYr = Xr * Yr, XY = X * Y;
         mxy.fremove(XYr);
         mx.fremove(Xr);
@@ -844,10 +906,10 @@ struct Corr {
     }
     // the pair starts at p = 1 (day 0's returns are NaN): min(p, W) pairs in the window, the
     // first remove at W + 1; removes of 0 before it are exact no-ops on the Kahan means
-    __device__ void wstep(Step& s) {
+    template <class S> __device__ void wstep(S& s) {
         const bool rm = s.p >= W + 1, ad = s.p >= 1;
         const int n = s.p >= W ? W : s.p;
-        const double Xr = rm ? s.fret(W) : 0.0, Yr = rm ? s.fvolchg(W) : 0.0;
+        const double Xr = rm ? s.template fret<W>() : 0.0, Yr = rm ? s.template fvolchg<W>() : 0.0;
         const double X = ad ? s.r0 : 0.0, Y = ad ? s.g0 : 0.0;
         const double XYr = Xr * Yr, XY = X * Y;
         mxy.wstep(XYr, XY, n);
@@ -893,25 +955,39 @@ struct Pack;
 template <>
 struct Pack<> {
     static constexpr unsigned kSer = 0;
+    static constexpr u64 kC = 0, kV = 0;
     __device__ void init() {}
     __device__ void step(Step&) {}
-    __device__ void fstep(Step&) {}
-    __device__ void wstep(Step&) {}
+    template <class S> __device__ void fstep(S&) {}
+    template <class S> __device__ void wstep(S&) {}
 };
 template <class H, class... R>
 struct Pack<H, R...> {
     static constexpr unsigned kSer = Ser<H>::value | Pack<R...>::kSer;
+    // the lookbacks the jobs' clean / warm steps read
+    static constexpr u64 kC = H::kC | Pack<R...>::kC, kV = H::kV | Pack<R...>::kV;
     H h;
     Pack<R...> r;
     __device__ void init() { h.init(); r.init(); }
-    __device__ void step(Step& s) { h.step(s); r.step(s); }
-    __device__ void fstep(Step& s) {
+    // the general step (cold) runs its jobs one after the other: interleaving them would raise
+    // the register pressure of the whole scan
+    __device__ void step(Step& s) {
+        h.step(s);
+        __builtin_amdgcn_sched_barrier(0);
+        r.step(s);
+    }
+    template <class S> __device__ void fstep(S& s) {
         h.fstep(s);     // no scheduling barrier: the compiler interleaves the jobs' independent
         r.fstep(s);     // chains (12.55 -> 12.32 ms at config C, bit-identical)
     }
-    __device__ void wstep(Step& s) { h.wstep(s); r.wstep(s); }
+    template <class S> __device__ void wstep(S& s) {
+        h.wstep(s);
+        __builtin_amdgcn_sched_barrier(0);
+        r.wstep(s);
+    }
 };
 
+#if AFM_FP_SETS == 15
 // Static job partition over the 15 job waves of one workgroup (LPT on the per-job VALU count of
 // the compiled step: Corr ~550, RetSd5x15 ~360, VolSd5x15 ~290, BB ~220, VWMA ~170, RetSd3 /
 // VolSd3 / PvtObvPsy ~155, RSI ~115, SMA / MomAccelRocr ~100, MACD ~75, EMA ~60; ~620 per wave),
@@ -935,9 +1011,42 @@ using W11 = Pack<Vwma<10>, Vwma<22>, Rsi<14>, Sma<22>, Ema<22>>;
 using W12 = Pack<Corr<15, false>, Macd<30>>;
 using W13 = Pack<Bbands<20>, Vwma<34>, MomAccelRocr<38>, Sma<46>, Sma<6>>;
 using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>, Ema<6>>;
+#define AFM_FP_FOR_SETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
+    X(13) X(14)
+#else
+// 21 job sets: each rolling correlation alone on a wave, the other jobs grouped so that a set's
+// windows share lookbacks; per item type (7 sets) the waves at positions p and p + 4 share a
+// SIMD in both halves of the pair, so positions (0, 4), (1, 5), (2, 6) carry about the work of
+// position 3 (the heaviest set, beside the loader at position 7).  Fast-step VALU per job:
+// Corr ~260, RetSd5x15 ~190, VolSd5x15 ~140, RetSd3 ~100, Bbands ~80, Vwma ~65, VolSd3 ~65,
+// PvtObvPsy ~60, Rsi ~55, MomAccelRocr ~35, Sma ~25, Macd ~15, Ema ~8.
+using W0 = Pack<Bbands<14>, MomAccelRocr<14>, Sma<14>, Ema<14>>;
+using W1 = Pack<Bbands<20>, MomAccelRocr<20>, Sma<18>, Ema<18>>;
+using W2 = Pack<Bbands<26>, MomAccelRocr<26>, Sma<26>, Ema<26>>;
+using W3 = Pack<Corr<5, true>>;
+using W4 = Pack<Rsi<8>, Rsi<14>, Macd<30>>;
+using W5 = Pack<Vwma<10>, Vwma<18>, Ema<22>>;
+using W6 = Pack<Vwma<22>, Vwma<26>, Ema<34>>;
+using W7 = Pack<Bbands<32>, MomAccelRocr<32>, Sma<30>, Ema<30>>;
+using W8 = Pack<Bbands<38>, MomAccelRocr<38>, Sma<38>, Ema<38>>;
+using W9 = Pack<Bbands<44>, MomAccelRocr<44>, Sma<42>, Ema<42>>;
+using W10 = Pack<Corr<15, false>>;
+using W11 = Pack<Rsi<20>, Vwma<14>>;
+using W12 = Pack<Vwma<30>, Vwma<34>, Sma<34>>;
+using W13 = Pack<Vwma<38>, Vwma<42>, Sma<22>>;
+using W14 = Pack<Bbands<50>, MomAccelRocr<50>, Sma<50>, Ema<50>>;
+using W15 = Pack<Bbands<56>, MomAccelRocr<56>, Sma<46>, Ema<46>>;
+using W16 = Pack<RetSd3, Sma<6>, Ema<10>, Macd<18>>;
+using W17 = Pack<RetSd5x15, VolSd3>;
+using W18 = Pack<Vwma<46>, Vwma<50>, Macd<24>>;
+using W19 = Pack<VolSd5x15, Ema<6>>;
+using W20 = Pack<PvtObvPsy, Vwma<6>, Sma<10>>;
+#define AFM_FP_FOR_SETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
+    X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)
+#endif
 
 // The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
-// job waves (one per chunk + two at each 64-day word end).  It also publishes, per lane and
+// job waves (one per chunk).  It also publishes, per lane and
 // chunk, whether every present day of the chunk is clean (kClean).
 __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane, int64_t block,
                                           GLB double* st) {
@@ -999,8 +1108,6 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
             stage(ch + 1);
             if (ch + 2 < nch) load(ch + 2);
         }
-        const int sh = (ch * kChunk) & 63;
-        if (sh + kChunk == 64 || ch + 1 == nch) { lds_barrier(); lds_barrier(); }
         lds_barrier();
     }
     if (st) {                                       // for the next slab (after the last barrier:
@@ -1018,11 +1125,7 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
 __device__ __forceinline__ void idle_wave(const Args& a) {
     const int nch = a.c1;
     lds_barrier();
-    for (int ch = a.c0; ch < nch; ++ch) {
-        const int sh = (ch * kChunk) & 63;
-        if (sh + kChunk == 64 || ch + 1 == nch) { lds_barrier(); lds_barrier(); }
-        lds_barrier();
-    }
+    for (int ch = a.c0; ch < nch; ++ch) lds_barrier();
 }
 
 // A job wave's complete state between two time slabs (stored lane-interleaved, 8-B words)
@@ -1049,11 +1152,16 @@ template <class P>
 __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type, int wave, int lane,
                                       int64_t block, GLB double* stp) {
     LDS Smem& sm = *smp;
-    const int64_t asset = block * kLanes + lane;
+    // this lane's byte offset inside a date row: every output / mask store is an SGPR row base
+    // plus this offset (no 64-bit per-lane address kept live through the scan)
+    const uint32_t voff = (uint32_t)((block * kLanes + lane) * 8);
     const int c0 = a.c0, nch = a.c1;
     const int64_t w0 = ((int64_t)c0 * kChunk) >> 6;                     // the slab's first word
-    const int64_t nwords = (a.t1 + 63) / 64 - w0;
     constexpr unsigned S = P::kSer;
+    // clean / warm steps: the pack's lookbacks, plus close 1 back for the returns and volume 1
+    // back for vol_change
+    constexpr u64 CM = P::kC | lb(0) | ((S & (kSerR | kSerXY)) ? lb(1) : 0ull);
+    constexpr u64 VM = P::kV | lb(0) | ((S & kSerXY) ? lb(1) : 0ull);
     P jobs;
     jobs.init();
     Runs rn;
@@ -1076,51 +1184,69 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     long long twait = 0;
 #endif
 
-    for (int ch = c0; ch < nch; ++ch) {
-        const int sh = (ch * kChunk) & 63;                 // chunk offset inside its word
-        const u64 cb = (u64)(unsigned)sm.cbyte[ch & 1][lane];
-        const int okl = sm.okbyte[ch & 1][lane];
-        const bool clean = __builtin_amdgcn_ballot_w64(okl != 2) == 0ull;
-        const bool warm = __builtin_amdgcn_ballot_w64(okl == 0) == 0ull;
-        const int64_t t0 = (int64_t)ch * kChunk;
+    FastStep<CM, VM> st;
+    st.sm = smp;
+    st.rn = &rn;
+    st.plane = a.plane;
+    st.voff = voff;
+    st.lane = lane;
+    // The steps of chunk ch over its present days, on one of the three paths (uniform in the wave).
+    auto fast_chunk = [&](int ch, unsigned cb, unsigned& n8, unsigned& f8) {
+        GLB double* row = a.out + (int64_t)ch * kChunk * a.lda;    // the chunk's first date row
         int p = pos, pm = pmod;
-        Step st;
-        st.sm = smp;
-        st.rn = &rn;
-        st.plane = a.plane;
-        st.voff = (uint32_t)(asset * 8);
-        st.lane = lane;
 #pragma unroll 1
-        for (int s = 0; s < kChunk; ++s) {
-            if ((cb >> s) & 1ull) {
-                st.out = a.out + (t0 + s) * a.lda;
+        for (int s = 0; s < kChunk; ++s, row += a.lda) {
+            if (cb & (1u << s)) {
+                st.out = row;
                 st.p = p;
                 st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
                 st.anynan = false;
                 st.anybad = false;
-                const double c0 = st.C(0), v0 = st.V(0);
-                if (clean) {
-                    if (S & (kSerR | kSerXY)) st.r0 = c0 / st.C(1) - 1;
-                    if (S & kSerXY) st.g0 = v0 / st.V(1) - 1;
-                    if (S & kSerC) rn.C.fupd(c0);
-                    if (S & kSerV) rn.V.fupd(v0);
-                    if (S & kSerVP) rn.VP.fupd(v0);
-                    if (S & kSerVC) rn.VC.fupd(v0 * c0);
-                    if (S & kSerR) rn.R.fupd(st.r0);
-                    if (S & kSerXY) {
-                        rn.X.fupd(st.r0);
-                        rn.Y.fupd(st.g0);
-                        rn.XY.fupd(st.r0 * st.g0);
-                    }
-                    jobs.fstep(st);
-                } else if (warm) {
-                    // warm-up windows: every observation of the lane so far in range (the first
-                    // kClean of a listing); the fast cores with the counts of a filling window.
-                    // Before p = 57 the row holds NaN (ACCEL_56), so the masks need no per-column
-                    // tracking there; from p = 57 the lane is clean and the fast columns' own
-                    // tracking applies.
-                    st.r0 = c0 / st.C(1) - 1;      // day 0: unused (no return yet)
-                    st.g0 = v0 / st.V(1) - 1;
+                st.gather();                          // every ring read of the step, then compute
+                __builtin_amdgcn_sched_barrier(0);
+                const double c0 = st.template c<0>(), v0 = st.template v<0>();
+                if constexpr ((S & (kSerR | kSerXY)) != 0) st.r0 = c0 / st.template c<1>() - 1;
+                if constexpr ((S & kSerXY) != 0) st.g0 = v0 / st.template v<1>() - 1;
+                if (S & kSerC) rn.C.fupd(c0);
+                if (S & kSerV) rn.V.fupd(v0);
+                if (S & kSerVP) rn.VP.fupd(v0);
+                if (S & kSerVC) rn.VC.fupd(v0 * c0);
+                if (S & kSerR) rn.R.fupd(st.r0);
+                if (S & kSerXY) {
+                    rn.X.fupd(st.r0);
+                    rn.Y.fupd(st.g0);
+                    rn.XY.fupd(st.r0 * st.g0);
+                }
+                jobs.fstep(st);
+                n8 |= st.anynan ? 1u << s : 0u;
+                f8 |= st.anybad ? 1u << s : 0u;
+                ++p;
+                pm = pm + 1 == kRing ? 0 : pm + 1;
+            }
+        }
+        pos = p;
+        pmod = pm;
+    };
+    auto slow_chunk = [&](int ch, unsigned cb, bool warm, unsigned& n8, unsigned& f8) {
+        GLB double* row = a.out + (int64_t)ch * kChunk * a.lda;
+        int p = pos, pm = pmod;
+        if (warm) {
+            // warm-up windows: every observation of the lane so far in range (the first kClean of
+            // a listing); the fast cores with the counts of a filling window.  Before p = 57 the
+            // row holds NaN (ACCEL_56), so the masks need no per-column tracking there; from
+            // p = 57 the lane is clean and the fast columns' own tracking applies.
+#pragma unroll 1
+            for (int s = 0; s < kChunk; ++s, row += a.lda) {
+                if (cb & (1u << s)) {
+                    st.out = row;
+                    st.p = p;
+                    st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
+                    st.gather();
+                    __builtin_amdgcn_sched_barrier(0);
+                    const double c0 = st.template c<0>(), v0 = st.template v<0>();
+                    // day 0: unused (no return yet)
+                    if constexpr ((S & (kSerR | kSerXY)) != 0) st.r0 = c0 / st.template c<1>() - 1;
+                    if constexpr ((S & kSerXY) != 0) st.g0 = v0 / st.template v<1>() - 1;
                     st.anynan = st.anybad = p < kClean - 1;
                     if (S & kSerC) rn.C.fupd(c0);
                     if (S & kSerV) rn.V.fupd(v0);
@@ -1135,7 +1261,22 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                         }
                     }
                     jobs.wstep(st);
-                } else {
+                    n8 |= st.anynan ? 1u << s : 0u;
+                    f8 |= st.anybad ? 1u << s : 0u;
+                    ++p;
+                    pm = pm + 1 == kRing ? 0 : pm + 1;
+                }
+            }
+        } else {
+#pragma unroll 1
+            for (int s = 0; s < kChunk; ++s, row += a.lda) {
+                if (cb & (1u << s)) {
+                    st.out = row;
+                    st.p = p;
+                    st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
+                    st.anynan = false;
+                    st.anybad = false;
+                    const double c0 = st.C(0), v0 = st.V(0);
                     if (S & (kSerR | kSerXY)) {
                         const double r = c0 / st.C(1) - 1;
                         st.r0 = p >= 1 ? r : qnan();
@@ -1156,29 +1297,28 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                         rn.XY.upd(X * Y);
                     }
                     jobs.step(st);
+                    n8 |= st.anynan ? 1u << s : 0u;
+                    f8 |= st.anybad ? 1u << s : 0u;
+                    ++p;
+                    pm = pm + 1 == kRing ? 0 : pm + 1;
                 }
-                if (st.anynan) nb |= 1ull << (sh + s);
-                if (st.anybad) fb |= 1ull << (sh + s);
-                ++p;
-                pm = pm + 1 == kRing ? 0 : pm + 1;
             }
         }
         pos = p;
         pmod = pm;
-        if (sh + kChunk == 64 || ch + 1 == nch) {          // word end: uniform in the workgroup
-            if (wave == 0) { sm.nanmask[lane] = nb; sm.badmask[lane] = fb; }
-            lds_barrier();
-            if (wave != 0) {
-                if (nb) __atomic_fetch_or(&sm.nanmask[lane], nb, __ATOMIC_RELAXED);
-                if (fb) __atomic_fetch_or(&sm.badmask[lane], fb, __ATOMIC_RELAXED);
-            }
-            lds_barrier();
-            if (wave == 0) {
-                const int64_t o = ((int64_t)type * nwords + (((int64_t)(ch * kChunk) >> 6) - w0))
-                                  * a.lda + asset;
-                a.nanpart[o] = sm.nanmask[lane];
-                a.badpart[o] = sm.badmask[lane];
-            }
+    };
+    // chunk ch done: its day bits into the word masks, stored at each word end (masks_kernel
+    // ORs the job waves' partials); then the chunk barrier
+    auto chunk_end = [&](int ch, unsigned n8, unsigned f8) {
+        const int sh = (ch * kChunk) & 63;                 // chunk offset inside its word
+        nb |= (u64)n8 << sh;
+        fb |= (u64)f8 << sh;
+        if (sh + kChunk == 64 || ch + 1 == nch) {          // word end: this wave's partial words
+            // SGPR row base + lane offset, as the output stores (a compiler-visible store here
+            // would make it drain the wave's output stores before reusing the registers)
+            const int64_t wrow = (((int64_t)(ch * kChunk) >> 6) - w0) * a.lda;
+            asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(nb), "s"(a.nanpart + wrow));
+            asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(fb), "s"(a.badpart + wrow));
             nb = 0ull;
             fb = 0ull;
         }
@@ -1189,6 +1329,39 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
 #else
         lds_barrier();
 #endif
+    };
+    int ch = c0;
+    auto is_clean = [&](int c) {
+        return __builtin_amdgcn_ballot_w64(sm.okbyte[c & 1][lane] != 2) == 0ull;
+    };
+    while (ch < nch) {
+        if (is_clean(ch)) {
+            // a run of chunks that are clean for the whole wave.  Its first chunk is peeled off
+            // the hot loop and followed by a vmcnt(0): a register whose load (a spill reload of
+            // the slow paths, the state restore) is still in flight at a loop head makes the
+            // compiler wait on vmcnt inside that loop -- and vmcnt counts this wave's output
+            // stores too, so that wait would drain them on every step
+            {
+                unsigned n8 = 0u, f8 = 0u;
+                fast_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], n8, f8);
+                chunk_end(ch, n8, f8);
+                ++ch;
+            }
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            while (ch < nch && is_clean(ch)) {              // the hot loop
+                unsigned n8 = 0u, f8 = 0u;
+                fast_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], n8, f8);
+                chunk_end(ch, n8, f8);
+                ++ch;
+            }
+        } else {                                            // one warm or general chunk
+            const int okl = sm.okbyte[ch & 1][lane];
+            const bool warm = __builtin_amdgcn_ballot_w64(okl == 0) == 0ull;
+            unsigned n8 = 0u, f8 = 0u;
+            slow_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], warm, n8, f8);
+            chunk_end(ch, n8, f8);
+            ++ch;
+        }
     }
     if (stp) {
         JobState<P> js;
@@ -1215,11 +1388,12 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
 // words of one wave's slab-carry state (the largest job set's JobState, or a loader's ring)
 template <class P> constexpr int state_words() { return (int)((sizeof(JobState<P>) + 7) / 8); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-constexpr int kStateWords = cmax(cmax(cmax(cmax(state_words<W0>(), state_words<W1>()),
-    cmax(state_words<W2>(), state_words<W3>())), cmax(cmax(state_words<W4>(), state_words<W5>()),
-    cmax(state_words<W6>(), state_words<W7>()))), cmax(cmax(cmax(state_words<W8>(),
-    state_words<W9>()), cmax(state_words<W10>(), state_words<W11>())), cmax(cmax(
-    state_words<W12>(), state_words<W13>()), cmax(state_words<W14>(), 2 * kRing + 3))));
+#define AFM_FP_STATE_WORDS(k) cmax(state_words<W##k>(),
+constexpr int kStateWords = AFM_FP_FOR_SETS(AFM_FP_STATE_WORDS) 2 * kRing + 3
+#define AFM_FP_CLOSE(k) )
+    AFM_FP_FOR_SETS(AFM_FP_CLOSE);
+#undef AFM_FP_STATE_WORDS
+#undef AFM_FP_CLOSE
 
 // TYPES workgroups per block, each with J = 15 / TYPES job waves (job sets W[J*type + wave]) and
 // a loader wave.  PAIR: one workgroup runs TWO such items (two rings, 2 x (J + 1) waves), items
@@ -1231,14 +1405,30 @@ constexpr int kStateWords = cmax(cmax(cmax(cmax(state_words<W0>(), state_words<W
 // Wave w of a workgroup issues on SIMD w % 4; the layouts minimise the busiest SIMD's measured
 // cycles (tools/wave_profile.py; type 1: 61.3 -> 55.0 Mcycles; round 2 re-checked for the new
 // partition with AFM_FP_LAYOUT, tools/gpu_layout.sh: four other layouts per type, none faster).
+#if AFM_FP_SETS == 15
 __constant__ signed char kPairLayout[3][2][6] = {
     {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
     {{0, 2, 3, 4, 1, 5}, {1, 2, 3, 4, 0, 5}},
     {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
 };
+#else
+// the partition above is ordered by position already (loader at position 7)
+__constant__ signed char kPairLayout[3][2][8] = {
+    {{0, 1, 2, 3, 4, 5, 6, 7}, {0, 1, 2, 3, 4, 5, 6, 7}},
+    {{0, 1, 2, 3, 4, 5, 6, 7}, {0, 1, 2, 3, 4, 5, 6, 7}},
+    {{0, 1, 2, 3, 4, 5, 6, 7}, {0, 1, 2, 3, 4, 5, 6, 7}},
+};
+#endif
+// waves per SIMD a launch shape needs resident (the VGPR budget): the paired 3-way launch fills
+// the CU's four SIMDs evenly; the other splits allow 2 (256 VGPRs)
+template <int TYPES, bool PAIR>
+constexpr int waves_per_simd() {
+    constexpr int w = (kJobSets / TYPES + 1) * (PAIR ? 2 : 1);
+    return w >= 12 ? (w + 3) / 4 : 2;
+}
 
 template <int TYPES, bool PAIR>
-__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1) * (PAIR ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(TYPES == 1 ? 4 : TYPES == 3 ? 3 : 2)))
+__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1) * (PAIR ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(waves_per_simd<TYPES, PAIR>())))
 void factor_panel_kernel(Args a) {
     constexpr int J = kJobSets / TYPES;
     // dynamic LDS: with a static size the compiler pads the VGPR allocation of the split
@@ -1272,28 +1462,17 @@ void factor_panel_kernel(Args a) {
     // this type's partial-mask planes (keeps the type out of the job waves' registers)
     Args at = a;
     const int64_t w0 = ((int64_t)a.c0 * kChunk) >> 6;
-    const int64_t po = (int64_t)type * ((a.t1 + 63) / 64 - w0) * a.lda;
+    const int64_t po = (int64_t)(type * J + wave) * ((a.t1 + 63) / 64 - w0) * a.lda;
     at.nanpart = a.nanpart + po;
     at.badpart = a.badpart + po;
 #ifdef AFM_FP_PROFILE
     at.pslot = (int)(block * TYPES + type);          // profile slot of this item
 #endif
     switch (type * J + wave) {
-        case 0: run_wave<W0>(at, sm, 0, wave, lane, block, stp); break;
-        case 1: run_wave<W1>(at, sm, 0, wave, lane, block, stp); break;
-        case 2: run_wave<W2>(at, sm, 0, wave, lane, block, stp); break;
-        case 3: run_wave<W3>(at, sm, 0, wave, lane, block, stp); break;
-        case 4: run_wave<W4>(at, sm, 0, wave, lane, block, stp); break;
-        case 5: run_wave<W5>(at, sm, 0, wave, lane, block, stp); break;
-        case 6: run_wave<W6>(at, sm, 0, wave, lane, block, stp); break;
-        case 7: run_wave<W7>(at, sm, 0, wave, lane, block, stp); break;
-        case 8: run_wave<W8>(at, sm, 0, wave, lane, block, stp); break;
-        case 9: run_wave<W9>(at, sm, 0, wave, lane, block, stp); break;
-        case 10: run_wave<W10>(at, sm, 0, wave, lane, block, stp); break;
-        case 11: run_wave<W11>(at, sm, 0, wave, lane, block, stp); break;
-        case 12: run_wave<W12>(at, sm, 0, wave, lane, block, stp); break;
-        case 13: run_wave<W13>(at, sm, 0, wave, lane, block, stp); break;
-        default: run_wave<W14>(at, sm, 0, wave, lane, block, stp); break;
+#define AFM_FP_CASE(k) case k: run_wave<W##k>(at, sm, 0, wave, lane, block, stp); break;
+        AFM_FP_FOR_SETS(AFM_FP_CASE)
+#undef AFM_FP_CASE
+        default: break;
     }
 }
 
@@ -1410,10 +1589,37 @@ static int factor_types(afm_ctx* ctx, int64_t nblk) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
         ncu = 256;
     int types = 3;
+#if AFM_FP_SETS == 15
     for (int t : {5, 15})
+#else
+    for (int t : {7, 21})
+#endif
         if (nblk * t <= 2 * (int64_t)ncu) types = t;
     if (ctx->factor_split) types = ctx->factor_split;              // option factor_split
     return types;
+}
+
+// a split of the kJobSets job waves over TYPES workgroups per block: J job waves + a loader
+static constexpr bool split_ok(int types) {
+    return types >= 1 && afm::kJobSets % types == 0 && afm::kJobSets / types + 1 <= 16;
+}
+template <int TYPES, bool PAIR>
+static int launch_split(afm_ctx* ctx, int64_t nblk, const afm::Args& a) {
+    if constexpr (!split_ok(TYPES)) {
+        (void)ctx; (void)nblk; (void)a;
+        afm_set_error("factor kernel: factor_split is not a split of the job sets");
+        return AFM_E_ARG;
+    } else {
+        constexpr int J = afm::kJobSets / TYPES;
+        const int bytes = (int)sizeof(afm::Smem) * (PAIR ? 2 : 1);    // > 64 KB: opt in
+        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<TYPES, PAIR>, bytes));
+        const int64_t items = nblk * TYPES;
+        const dim3 grid((unsigned)(PAIR ? (items + 1) / 2 : items));
+        hipLaunchKernelGGL((afm::factor_panel_kernel<TYPES, PAIR>), grid,
+                           dim3(64 * (J + 1) * (PAIR ? 2 : 1)), bytes, ctx->stream, a);
+        AFM_HIP(hipGetLastError());
+        return AFM_OK;
+    }
 }
 
 // The factor kernel over the time slab [t0, t1) of the [T]-date series (t0 a multiple of 64;
@@ -1426,8 +1632,8 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     const int64_t nwords = (t1 - t0 + 63) / 64;                   // the slab's mask words
     const int64_t nblk = (A + 63) / 64;
     const int types = factor_types(ctx, nblk);
-    uint64_t* part = nullptr;
-    AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * types * nwords * lda,
+    uint64_t* part = nullptr;         // per-job-wave mask partials (masks_kernel ORs them)
+    AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * afm::kJobSets * nwords * lda,
                            ctx->stream));
     afm::Args a;
     a.T = T;
@@ -1438,7 +1644,7 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     a.vbits = (const GLB uint64_t*)valid_bits;
     a.out = (GLB double*)(out - t0 * lda);        // date t's row at a.out + t * lda
     a.nanpart = (GLB uint64_t*)part;
-    a.badpart = (GLB uint64_t*)(part + types * nwords * lda);
+    a.badpart = (GLB uint64_t*)(part + afm::kJobSets * nwords * lda);
     a.types = types;
     a.nblk = (int)nblk;
     a.pslot = 0;
@@ -1452,39 +1658,30 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     // factor_pair / factor_fast: the invariance tests' A/B
     const bool pair = ctx->factor_pair != 0;
     a.fast = ctx->factor_fast ? 1 : 0;
-    const dim3 grid((unsigned)(nblk * types));
-    {                                                 // > 64 KB of dynamic LDS: opt in
-        const int bytes = (int)sizeof(afm::Smem);
-        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<1, false>, bytes));
-        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<3, false>, bytes));
-        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<3, true>, 2 * bytes));
-        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<5, false>, bytes));
-        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<15, false>, bytes));
+    int rc;
+    switch (types) {                 // paired 2-item workgroups for the 3-way split (see the kernel)
+        case 1: rc = launch_split<1, false>(ctx, nblk, a); break;
+        case 3: rc = pair ? launch_split<3, true>(ctx, nblk, a) : launch_split<3, false>(ctx, nblk, a);
+                break;
+        case 5: rc = launch_split<5, false>(ctx, nblk, a); break;
+        case 7: rc = launch_split<7, false>(ctx, nblk, a); break;
+        case 15: rc = launch_split<15, false>(ctx, nblk, a); break;
+        case 21: rc = launch_split<21, false>(ctx, nblk, a); break;
+        default:
+            afm_set_error("factor kernel: factor_split is not a split of the job sets");
+            rc = AFM_E_ARG;
     }
-    switch (types) {
-        case 1: hipLaunchKernelGGL((afm::factor_panel_kernel<1, false>), grid, dim3(64 * 16),
-                                   sizeof(afm::Smem), ctx->stream, a); break;
-        case 3:
-            if (pair)
-                hipLaunchKernelGGL((afm::factor_panel_kernel<3, true>),
-                                   dim3((unsigned)((nblk * 3 + 1) / 2)), dim3(64 * 12),
-                                   2 * sizeof(afm::Smem), ctx->stream, a);
-            else
-                hipLaunchKernelGGL((afm::factor_panel_kernel<3, false>), grid, dim3(64 * 6),
-                                   sizeof(afm::Smem), ctx->stream, a);
-            break;
-        case 5: hipLaunchKernelGGL((afm::factor_panel_kernel<5, false>), grid, dim3(64 * 4),
-                                   sizeof(afm::Smem), ctx->stream, a); break;
-        default: hipLaunchKernelGGL((afm::factor_panel_kernel<15, false>), grid, dim3(64 * 2),
-                                    sizeof(afm::Smem), ctx->stream, a); break;
+    if (rc != AFM_OK) {
+        (void)hipFreeAsync(part, ctx->stream);
+        return rc;
     }
     AFM_HIP(hipGetLastError());
     const int64_t nw = nwords * lda;
     // columns past A (lda padding) carry no presence: their mask words come from valid_bits
     // (zero there), and the factor kernel never ran on blocks past ceil(A/64)
     hipLaunchKernelGGL(afm::masks_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0,
-                       ctx->stream, nwords, lda, types, valid_bits + (t0 / 64) * lda, part,
-                       part + types * nw, nanfree_bits, finite_bits);
+                       ctx->stream, nwords, lda, afm::kJobSets, valid_bits + (t0 / 64) * lda, part,
+                       part + afm::kJobSets * nw, nanfree_bits, finite_bits);
     AFM_HIP(hipGetLastError());
     if (excess) {                  // NULL: the caller runs afm_labels_f64 (e.g. on another stream)
         dim3 g2((unsigned)((lda + 255) / 256), (unsigned)((t1 - 1) / 64 - t0 / 64 + 1));

@@ -152,8 +152,8 @@ def test_stream_placement_bit_identical(chain_a, env, monkeypatch):
 
 def test_early_fm_identical_to_one_pass():
     """The per-date FM Grams computed early over the factor rows, then only the blocks holding a
-    z-score-dropped asset recomputed over the z-score rows (PipelineConfig.fm_early, the default
-    on one GPU), equal one pass over the z-score rows bit for bit -- on a panel where two assets
+    z-score-dropped asset recomputed over the z-score rows (PipelineConfig.fm_early; one GPU only,
+    off by default), equal one pass over the z-score rows bit for bit -- on a panel where two assets
     (in different blocks) drop out of the z-score: one constant-price asset (zero variance), one
     listed only after the train window (no train rows)."""
     import torch
@@ -167,7 +167,7 @@ def test_early_fm_identical_to_one_pass():
     p.valid[:1100, late] = False                         # listed after the train window
     grid = afm.PanelGrid.from_panel(p)
     cfg = dict(train_end="2003-12-31", valid_end="2004-06-30", window=60, top_n=10)
-    a = Pipeline(grid, PipelineConfig(**cfg))
+    a = Pipeline(grid, PipelineConfig(fm_early=True, **cfg))
     a.step()
     b = Pipeline(grid, PipelineConfig(fm_early=False, **cfg))
     b.step()
