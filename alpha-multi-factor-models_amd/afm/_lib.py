@@ -70,9 +70,6 @@ SIGNATURES = {
                             I64, P, I32]),
     "afm_zpool_f64": (I32, [P, P, I64, I64, P, P, I32, I32, P, I32, P, I64, I64, I64, I32, I64,
                             I32, P, I32]),
-    "afm_zgram_select_f64": (I32, [P, P, I64, I64, P, P, I32, I32, P, I32, P, I64, I64, I32, I64,
-                                   I64, I64, P, I32, P]),
-    "afm_block_flags": (I32, [P, P, I64, I32, I64, P]),
     "afm_gram_tree_f64": (I32, [P, I32, P, I64, I32, I32, P]),
     "afm_zpredict_f64": (I32, [P, P, I64, I64, I64, I64, P, I32, P, P, P, P]),
     "afm_lasso_fit_f64": (I32, [P, P, P, I32, DBL, I32, DBL, I32, P, P]),

@@ -100,13 +100,6 @@ class PipelineConfig:
     # variant may name another subset -- e.g. DENSE_FEATURES, which drops tmr_ret1d (the
     # undemeaned twin of the target, NT:90-91) so the Lasso keeps many coefficients
     features: tuple | None = None
-    # True (one GPU): the per-date FM Grams run right after the factor kernel, beside the z-score
-    # statistics, over the factor rows (frows); once the z-score rows exist, only the blocks that
-    # hold a dropped asset are recomputed (afm_zgram_select_f64) -- the same partials as one pass
-    # over the z-score rows.  Measured slower (46.2 vs 35.5 ms/step at config C: the FM MFMA
-    # Grams then share the SIMDs with the z statistics and the pooled Gram, 12.0 -> 19.6 ms), so
-    # the default is one pass after the predict.
-    fm_early: bool = False
 
 
 @dataclass
@@ -352,8 +345,6 @@ class Pipeline:
         self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
         self.labels_done = torch.cuda.Event()
-        self.frows_done = torch.cuda.Event()
-        self.fm_flags = torch.zeros(self.nblk_r, **i32)   # blocks holding a z-score-dropped asset
 
     def n_asset_days_local(self) -> int:
         return int(self.g.valid.sum().item())
@@ -391,28 +382,18 @@ class Pipeline:
         chk(L.afm_gram_tree_f64(h, p, P(self.te_part), self.nblk_r, self.nblk_r, 0,
                                 P(self.pool_blk[self.nblk_r:])), "tree date")
 
-    def _fm_local(self, h, stage="all"):
-        """This shard's per-date FM30 partials, merged over its blocks -> fm_sub [T].
-        stage "all": one pass over the z-score rows; "early": every block over the factor rows
-        (frows, before the z-score exists); "fix": the blocks flagged in fm_flags over the z-score
-        rows, then the tree."""
+    def _fm_local(self, h):
+        """This shard's per-date FM30 partials over the z-score rows, merged over its blocks ->
+        fm_sub [T]."""
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
         T, lda, pf = self.T, self.lda_r, self.pf
         if self.nrb == 0:
             return
-        if stage in ("all", "early"):
-            rows = self.zrows if stage == "all" else self.frows
-            chk(L.afm_zgram_f64(h, P(self.out), T * lda, lda, P(self.fm_cols), None, pf, TARGET,
-                                None, 0, P(rows), 0, T, self.nblk_r, 0, self.blk, self.A_r,
-                                P(self.fm_part), 0), "zgram fm")
-        if stage == "fix":
-            chk(L.afm_zgram_select_f64(h, P(self.out), T * lda, lda, P(self.fm_cols), None, pf,
-                                       TARGET, None, 0, P(self.zrows), 0, T, self.nblk_r, 0,
-                                       self.blk, self.A_r, P(self.fm_part), 0, P(self.fm_flags)),
-                "zgram fm fix")
-        if stage in ("all", "fix"):
-            chk(L.afm_gram_tree_f64(h, pf, P(self.fm_part), T * self.nblk_r, self.nblk_r, 0,
-                                    P(self.fm_sub)), "tree fm blocks")
+        chk(L.afm_zgram_f64(h, P(self.out), T * lda, lda, P(self.fm_cols), None, pf, TARGET,
+                            None, 0, P(self.zrows), 0, T, self.nblk_r, 0, self.blk, self.A_r,
+                            P(self.fm_part), 0), "zgram fm")
+        chk(L.afm_gram_tree_f64(h, pf, P(self.fm_part), T * self.nblk_r, self.nblk_r, 0,
+                                P(self.fm_sub)), "tree fm blocks")
 
     def _fm_solve(self, h, sub):
         """Owned dates: the rank subtrees ``sub`` [fnd][W][part] -> Grams, solves; every rank then
@@ -465,18 +446,6 @@ class Pipeline:
                 chk(L.afm_drop_last_obs_bits(h, T, lda_r, P(g.vbits), P(self.finite),
                                              P(self.frows)), "finite rows")
             mark("factors", 1)
-            early = W == 1 and c.fm_early and self.A_r > 0
-            if early:        # per-date FM Grams over the factor rows, beside the z statistics
-                self.frows_done.record(self.main)
-                self.side.wait_event(self.frows_done)
-                if lab_side:
-                    self.side.wait_event(self.labels_done)      # the target plane
-                with torch.cuda.stream(self.side):
-                    hs = self.ctx.bind_stream()
-                    mark("fm", 0)
-                    self._fm_local(hs, "early")
-                    mark("fm", 1)
-                h = self.ctx.bind_stream()
             mark("zstats", 0)
             if self.A_r > 0:
                 if lab_side:
@@ -488,9 +457,6 @@ class Pipeline:
                                               P(self.asset_ok)), "zstats finalize")
                 chk(L.afm_row_bits(h, nch, lda_r, P(self.frows), None, P(self.asset_ok), 0, T,
                                    P(self.zrows)), "z rows")
-                if early:
-                    chk(L.afm_block_flags(h, P(self.asset_ok), self.A_r, self.nblk_r, self.blk,
-                                          P(self.fm_flags)), "fm block flags")
             mark("zstats", 1)
             if W > 1:           # full-width label planes for the rebalance, during the Grams
                 with torch.cuda.stream(self.side2):
@@ -532,14 +498,12 @@ class Pipeline:
                 self.side.wait_stream(self.main)
                 with torch.cuda.stream(self.side):
                     hs = self.ctx.bind_stream()
-                    if not early:
-                        mark("fm", 0)
-                    self._fm_local(hs, "fix" if early else "all")
+                    mark("fm", 0)
+                    self._fm_local(hs)
                     if W == 1:
                         self._fm_solve(hs, self.fm_sub)
                         self._fm_stats(hs)
-                    if not early:
-                        mark("fm", 1)
+                    mark("fm", 1)
                 return self.ctx.bind_stream()
 
             fm_at = os.environ.get("AFM_FM_FORK", "predict") if W == 1 else "gram"

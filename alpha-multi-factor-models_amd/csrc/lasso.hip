@@ -35,6 +35,17 @@ __device__ __forceinline__ double pick(double v0, double v1, int j) {
     return j < 64 ? bcast(v0, j) : bcast(v1, j - 64);
 }
 __device__ __forceinline__ double fsign(double f) { return f == 0.0 ? 0.0 : (f > 0.0 ? 1.0 : -1.0); }
+// x / d with r = RN(1 / d): Markstein's correction q0 = RN(x r), e = fma(-q0, d, x),
+// q = RN(q0 + e r) is the IEEE quotient when r is the correctly rounded reciprocal and nothing
+// under- or overflows (checked on 5.6e8 hard and random cases, tools/markstein_any.c); zero,
+// non-finite and tiny quotients take the IEEE division.
+__device__ __forceinline__ double div_r(double x, double d, double r) {
+    const double q0 = x * r;
+    const double e = __builtin_fma(-q0, d, x);
+    const double q1 = __builtin_fma(e, r, q0);
+    const double aq = __builtin_fabs(q0);
+    return (aq > 0x1p-400 && aq < 0x1p400) ? q1 : x / d;
+}
 
 // alpha_row >= 0: alpha = alpha_row * n (sklearn's alpha times the row count, read on the device);
 // shift / beta_out (optional): beta_out = [intercept, w] with sklearn's _set_intercept,
@@ -75,6 +86,12 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     // changes nothing (no H update, w stays a signed zero) -- the sweep skips to the next
     // coordinate that can move, found by ballot over the lanes' current H
     const double qd0 = has0 ? Q[j0 * p + j0] : 0.0, qd1 = has1 ? Q[j1 * p + j1] : 0.0;
+    // the soft-threshold divisors qii + beta and their correctly rounded reciprocals (a divisor
+    // whose reciprocal is not normal keeps the IEEE division: rd = 0 marks it)
+    const double dd0 = qd0 + beta, dd1 = qd1 + beta;
+    double rd0 = 1.0 / dd0, rd1 = 1.0 / dd1;
+    if (!(__builtin_fabs(rd0) > 0x1p-400 && __builtin_fabs(rd0) < 0x1p400)) rd0 = 0.0;
+    if (!(__builtin_fabs(rd1) > 0x1p-400 && __builtin_fabs(rd1) < 0x1p400)) rd1 = 0.0;
     auto movable = [&](double qd, double q, double h, double w) {
         const double tmp = q - h;
         const bool nz = (positive && tmp < 0) ? false : __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0) != 0.0;
@@ -100,18 +117,27 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
                 }
             }
             const double* row = Q + ii * p;
-            const double qii = row[ii];
+            const double qii = pick(qd0, qd1, ii);
             if (qii == 0.0) continue;
             const double r0 = has0 ? row[j0] : 0.0, r1 = has1 ? row[j1] : 0.0;
             const double w_ii = pick(w0, w1, ii);
+            // H[ii] after the first axpy is lane ii's own fma (r = Q[ii][ii] there): computed on
+            // the scalar path directly, so the step does not wait for the row read or the axpy
+            const double h_ii = pick(h0, h1, ii);
+            const double hh = w_ii != 0.0 ? __builtin_fma(-w_ii, qii, h_ii) : h_ii;
             if (w_ii != 0.0) {
                 h0 = __builtin_fma(-w_ii, r0, h0);
                 h1 = __builtin_fma(-w_ii, r1, h1);
             }
-            const double tmp = pick(q0, q1, ii) - pick(h0, h1, ii);
+            const double tmp = pick(q0, q1, ii) - hh;
             double wn;
-            if (positive && tmp < 0) wn = 0.0;
-            else wn = fsign(tmp) * __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0) / (qii + beta);
+            if (positive && tmp < 0) {
+                wn = 0.0;
+            } else {
+                const double num = fsign(tmp) * __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0);
+                const double rdi = pick(rd0, rd1, ii);
+                wn = rdi != 0.0 ? div_r(num, qii + beta, rdi) : num / (qii + beta);
+            }
             if (ii < 64) { if (lane == ii) w0 = wn; }
             else if (lane == ii - 64) w1 = wn;
             if (wn != 0.0) {

@@ -100,8 +100,6 @@ struct ZGramArgs {
     int nchunk;              // mode 1: date chunks of [t0, t0 + nt)
     double* part;            // mode 0: [nt][nblk][PE]; mode 1: [nrb][nchunk][PE]
     int even;                // pad every item to an even slot count (zgram_produce_pairs)
-    const int32_t* only;     // mode 0 (or null): only blocks b with only[b] != 0 -- the items of
-                             // the others are skipped and their partials left as they are
 };
 
 // The ring: nslots slots of (p + 4) LDS rows (rows 0..p+1 staged, row p+2 stays zero: the
@@ -139,10 +137,6 @@ struct Seq {
     int masked;              // an all-masked slot (empty chunk, or the padding slot)
     int k, kend, kreal;      // position inside the item (row-block or date); real slots < kreal
     __device__ void start(const ZGramArgs& g) {
-        if (g.mode == 0 && g.only) {             // skip the items of unselected blocks (every
-            while (item < nitems && !g.only[item % g.nblk]) item += stride;   // wave alike)
-            if (item >= nitems) return;
-        }
         if (g.mode == 0) {
             const int d = item / g.nblk, b = item - d * g.nblk;
             t = (int)g.t0 + d;
@@ -759,11 +753,12 @@ static int zgram_common_checks(const double* base, const int32_t* cols, const do
     return AFM_OK;
 }
 
-static int zgram_blocks(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
-                        const int32_t* cols, const int32_t* zcols, int p, int ycol,
-                        const double* zs, int zid, const uint64_t* bits, int64_t t0, int64_t nt,
-                        int nblk, int64_t blk0, int64_t blk_assets, int64_t a_end, double* part,
-                        int grid, const int32_t* only) {
+extern "C" int afm_zgram_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
+                             const int32_t* cols, const int32_t* zcols, int p, int ycol,
+                             const double* zs, int zid, const uint64_t* bits, int64_t t0,
+                             int64_t nt, int nblk, int64_t blk0, int64_t blk_assets,
+                             int64_t a_end, double* part, int grid) {
+    AFM_CTX(ctx);
     const int rc = zgram_common_checks(base, cols, zs, bits, part, p, lda, a_end, blk0, t0, nt);
     if (rc) return rc;
     AFM_CHECK_ARG(nblk >= 1 && blk_assets > 0 && blk_assets % 64 == 0 && nt * nblk < (1ll << 31),
@@ -772,56 +767,10 @@ static int zgram_blocks(afm_ctx* ctx, const double* base, int64_t col_stride, in
     // the two-tile shape (NT = 2) stages item pairs (zgram_produce_pairs): even slot counts
     const int even = (!zs || zgram_nt(p) == 2) ? 1 : 0;
     ZGramArgs g{base, col_stride, lda, cols, zcols, p, ycol, zid, zs, bits, t0, nt, 0, nblk, blk0,
-                blk_assets, a_end, 0, 1, part, even, only};
+                blk_assets, a_end, 0, 1, part, even};
     if (!zs) return launch_zgram<2, 0, false>(ctx, g, nt * nblk, grid);   // FM: raw columns
     return zgram_nt(p) == 2 ? launch_zgram<2, 0, true>(ctx, g, nt * nblk, grid)
                             : launch_zgram<7, 0, true>(ctx, g, nt * nblk, grid);
-}
-
-extern "C" int afm_zgram_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
-                             const int32_t* cols, const int32_t* zcols, int p, int ycol,
-                             const double* zs, int zid, const uint64_t* bits, int64_t t0,
-                             int64_t nt, int nblk, int64_t blk0, int64_t blk_assets,
-                             int64_t a_end, double* part, int grid) {
-    AFM_CTX(ctx);
-    return zgram_blocks(ctx, base, col_stride, lda, cols, zcols, p, ycol, zs, zid, bits, t0, nt,
-                        nblk, blk0, blk_assets, a_end, part, grid, nullptr);
-}
-
-extern "C" int afm_zgram_select_f64(afm_ctx* ctx, const double* base, int64_t col_stride,
-                                    int64_t lda, const int32_t* cols, const int32_t* zcols, int p,
-                                    int ycol, const double* zs, int zid, const uint64_t* bits,
-                                    int64_t t0, int64_t nt, int nblk, int64_t blk0,
-                                    int64_t blk_assets, int64_t a_end, double* part, int grid,
-                                    const int32_t* only) {
-    AFM_CTX(ctx);
-    AFM_CHECK_ARG(only != nullptr, "only: the per-block selection is required");
-    return zgram_blocks(ctx, base, col_stride, lda, cols, zcols, p, ycol, zs, zid, bits, t0, nt,
-                        nblk, blk0, blk_assets, a_end, part, grid, only);
-}
-
-// flags[b] = 1 when block b = assets [b * blk, min((b + 1) * blk, a_end)) holds an asset with
-// asset_ok == 0 (one workgroup per block)
-__global__ __launch_bounds__(256) void afm_block_flags_kernel(const int32_t* asset_ok, int64_t a_end,
-                                                              int64_t blk, int32_t* flags) {
-    __shared__ int any;
-    if (threadIdx.x == 0) any = 0;
-    __syncthreads();
-    const int64_t b = blockIdx.x;
-    for (int64_t a = b * blk + threadIdx.x; a < (b + 1) * blk && a < a_end; a += 256)
-        if (!asset_ok[a]) any = 1;
-    __syncthreads();
-    if (threadIdx.x == 0) flags[b] = any;
-}
-
-extern "C" int afm_block_flags(afm_ctx* ctx, const int32_t* asset_ok, int64_t a_end, int nblk,
-                               int64_t blk, int32_t* flags) {
-    AFM_CTX(ctx);
-    AFM_CHECK_ARG(asset_ok && flags && nblk >= 1 && blk > 0, "bad arguments");
-    hipLaunchKernelGGL(afm_block_flags_kernel, dim3((unsigned)nblk), dim3(256), 0, ctx->stream,
-                       asset_ok, a_end, blk, flags);
-    AFM_HIP(hipGetLastError());
-    return AFM_OK;
 }
 
 extern "C" int afm_zpool_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
@@ -835,7 +784,7 @@ extern "C" int afm_zpool_f64(afm_ctx* ctx, const double* base, int64_t col_strid
     AFM_CHECK_ARG(nrb >= 0 && nchunk >= 1 && (int64_t)nrb * nchunk < (1ll << 31), "bad leaves");
     if (nrb == 0) return AFM_OK;
     ZGramArgs g{base, col_stride, lda, cols, zcols, p, ycol, zid, zs, bits, t0, nt, 1, 1, blk0,
-                64, a_end, nrb, nchunk, part, zgram_nt(p) == 2 ? 1 : 0, nullptr};
+                64, a_end, nrb, nchunk, part, zgram_nt(p) == 2 ? 1 : 0};
     AFM_CHECK_ARG(zs != nullptr, "afm_zpool_f64 needs zs");
     return zgram_nt(p) == 2 ? launch_zgram<2, 1, true>(ctx, g, (int64_t)nrb * nchunk, grid)
                             : launch_zgram<7, 1, true>(ctx, g, (int64_t)nrb * nchunk, grid);

@@ -27,21 +27,11 @@ constexpr int kUnroll = 8;
 
 __device__ __forceinline__ double qnan() { return __builtin_nan(""); }
 
-// rtab[n] = RN(1 / n) (rtab[0] unused): the Welford update divides by the observation count;
-// with the correctly rounded reciprocal, q0 = RN(x r), e = fma(-q0, n, x), RN(q0 + e r) is the
-// IEEE quotient (Markstein; tools/markstein_check.c checks every n <= 8192 on hard cases) in 3
-// VALU operations instead of the ~11 of the general division.
-__global__ __launch_bounds__(256) void recip_table_kernel(int64_t n, double* rtab) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i <= n) rtab[i] = i ? 1.0 / (double)i : 0.0;
-}
-
 // grid (ceil(lda / 256), K); thread = (column k = blockIdx.y, asset a)
 __global__ __launch_bounds__(256) void zscore_stats_kernel(const double* base, int64_t col_stride,
                                                            int64_t lda, const int32_t* cols,
                                                            const uint64_t* bits, int64_t t0,
-                                                           int64_t t1, const double* rtab,
-                                                           double* mu, double* sd) {
+                                                           int64_t t1, double* mu, double* sd) {
     const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int k = blockIdx.y;
     if (a >= lda) return;
@@ -50,8 +40,7 @@ __global__ __launch_bounds__(256) void zscore_stats_kernel(const double* base, i
     double sum = 0.0, comp = 0.0;
     // group_var: Welford
     double mean = 0.0, m2 = 0.0;
-    int nobs = 0;
-    double dn = 0.0;                                    // (double)nobs
+    int64_t nobs = 0;
     for (int64_t c = t0 >> 6; c <= (t1 - 1) >> 6; ++c) {
         u64 w = bits[c * lda + a];
         const int64_t d0 = c << 6;
@@ -70,27 +59,19 @@ __global__ __launch_bounds__(256) void zscore_stats_kernel(const double* base, i
                 const double val = v[j];
                 if (val == val) {                       // absent rows read NaN: skipped
                     nobs += 1;
-                    dn = dn + 1.0;
                     const double y = val - comp;
                     const double t = sum + y;
                     comp = t - sum - y;
                     if (comp != comp) comp = 0.0;
                     sum = t;
                     const double old = mean;
-                    const double dv = val - old, r = rtab[nobs];
-                    const double q0 = dv * r;
-                    double q;                            // zero / inf / NaN / tiny: IEEE divide
-                    if (__builtin_expect(__builtin_fabs(q0) >= 0x1p-1000 && __builtin_isfinite(q0), 1))
-                        q = __builtin_fma(__builtin_fma(-q0, dn, dv), r, q0);
-                    else
-                        q = dv / dn;
-                    mean = mean + q;                     // = mean + (val - old) / nobs
+                    mean = mean + (val - old) / (double)nobs;
                     m2 = m2 + (val - mean) * (val - old);
                 }
             }
         }
     }
-    const double ct = dn;
+    const double ct = (double)nobs;
     mu[(int64_t)k * lda + a] = nobs == 0 ? qnan() : sum / ct;
     sd[(int64_t)k * lda + a] = nobs <= 1 ? qnan() : __builtin_sqrt(m2 / (ct - 1.0));
 }
@@ -159,18 +140,10 @@ extern "C" int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t co
         AFM_HIP(hipMemsetAsync(sd, 0xff, sizeof(double) * K * lda, ctx->stream));
         return AFM_OK;
     }
-    // reciprocals of the observation counts 1 .. t1 - t0 (stream-ordered scratch)
-    const int64_t nmax = t1 - t0;
-    double* rtab = nullptr;
-    AFM_HIP(hipMallocAsync((void**)&rtab, sizeof(double) * (size_t)(nmax + 1), ctx->stream));
-    hipLaunchKernelGGL(recip_table_kernel, dim3((unsigned)((nmax + 256) / 256)), dim3(256), 0,
-                       ctx->stream, nmax, rtab);
-    AFM_HIP(hipGetLastError());
     dim3 grid((unsigned)((lda + 255) / 256), (unsigned)K);
     hipLaunchKernelGGL(zscore_stats_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride,
-                       lda, cols, bits, t0, t1, (const double*)rtab, mu, sd);
+                       lda, cols, bits, t0, t1, mu, sd);
     AFM_HIP(hipGetLastError());
-    AFM_HIP(hipFreeAsync(rtab, ctx->stream));
     return AFM_OK;
 }
 

@@ -312,20 +312,6 @@ int afm_zgram_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t 
                   const int32_t* cols, const int32_t* zcols, int p, int ycol, const double* zs,
                   int zid, const uint64_t* bits, int64_t t0, int64_t nt, int nblk, int64_t blk0,
                   int64_t blk_assets, int64_t a_end, double* part, int grid);
-/* afm_zgram_f64 restricted to the blocks b with only[b] != 0 (DEVICE int32 [nblk]): the other
- * blocks' partials are left untouched.  The early per-date FM Grams of a step are computed over
- * the factor rows before the z-score statistics exist; once they do, the blocks holding an asset
- * the z-score drops (afm_block_flags) are recomputed over the z-score rows -- the same partials
- * as a single pass over the z-score rows, bit for bit. */
-int afm_zgram_select_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
-                         const int32_t* cols, const int32_t* zcols, int p, int ycol,
-                         const double* zs, int zid, const uint64_t* bits, int64_t t0, int64_t nt,
-                         int nblk, int64_t blk0, int64_t blk_assets, int64_t a_end, double* part,
-                         int grid, const int32_t* only);
-/* flags[b] = 1 if block b (assets [b*blk, min((b+1)*blk, a_end))) holds an asset with
- * asset_ok == 0, else 0 (DEVICE int32 [nblk]). */
-int afm_block_flags(afm_ctx* ctx, const int32_t* asset_ok, int64_t a_end, int nblk, int64_t blk,
-                    int32_t* flags);
 int afm_zpool_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t lda,
                   const int32_t* cols, const int32_t* zcols, int p, int ycol, const double* zs,
                   int zid, const uint64_t* bits, int64_t t0, int64_t nt, int64_t blk0, int nrb,

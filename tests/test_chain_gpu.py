@@ -148,36 +148,3 @@ def test_stream_placement_bit_identical(chain_a, env, monkeypatch):
     for k in ("k", "books", "weights"):
         assert torch.equal(pipe.reb[k], other.reb[k]), k
     assert torch.equal(pipe.pnl["value"], other.pnl["value"])
-
-
-def test_early_fm_identical_to_one_pass():
-    """The per-date FM Grams computed early over the factor rows, then only the blocks holding a
-    z-score-dropped asset recomputed over the z-score rows (PipelineConfig.fm_early; one GPU only,
-    off by default), equal one pass over the z-score rows bit for bit -- on a panel where two assets
-    (in different blocks) drop out of the z-score: one constant-price asset (zero variance), one
-    listed only after the train window (no train rows)."""
-    import torch
-    import afm
-    from afm.pipeline import Pipeline, PipelineConfig
-    from afm.synthetic import make_panel
-    p = make_panel(700, 1300, seed=21, tradable_p=0.9)
-    p.close[:, 5] = 42.0                                 # flat: every price feature has sd = 0
-    p.ret1d[:, 5] = 0.0
-    late = 650
-    p.valid[:1100, late] = False                         # listed after the train window
-    grid = afm.PanelGrid.from_panel(p)
-    cfg = dict(train_end="2003-12-31", valid_end="2004-06-30", window=60, top_n=10)
-    a = Pipeline(grid, PipelineConfig(fm_early=True, **cfg))
-    a.step()
-    b = Pipeline(grid, PipelineConfig(fm_early=False, **cfg))
-    b.step()
-    torch.cuda.synchronize()
-    ok = a.asset_ok.cpu().numpy()
-    assert ok[5] == 0 and ok[late] == 0
-    flags = a.fm_flags.cpu().numpy()
-    assert flags[5 // a.blk] == 1 and flags[late // a.blk] == 1 and flags.sum() == 2
-    for name in ("fm_beta", "fm_nobs", "fm_mean", "fm_t"):
-        x, y = getattr(a, name), getattr(b, name)
-        assert torch.equal(x.view(torch.int64) if x.dtype == torch.float64 else x,
-                           y.view(torch.int64) if y.dtype == torch.float64 else y), name
-    assert torch.equal(a.fm_sub.view(torch.int64), b.fm_sub.view(torch.int64))

@@ -2,7 +2,7 @@
 """A/B of PipelineConfig switches on the config-C step, each variant in its own process (one
 Pipeline per process: two resident config-C pipelines slow the z-score and Gram stages), run in
 alternation.  Usage: python tools/stage_ab.py [--steps 10 --rounds 2] [--lib-b PATH]
-Default: fm_early=True vs fm_early=False (the default).  --lib-b: same config, library variant B (AFM_LIB)."""
+--lib-b: the same config on library variant B (AFM_LIB); without it, the default build alone."""
 import argparse
 import json
 import os
@@ -50,7 +50,7 @@ def main():
     if a.lib_b:
         variants = {"A": ({}, None), "B": ({}, a.lib_b)}
     else:
-        variants = {"fm_early": ({"fm_early": True}, None), "fm_late": ({}, None)}
+        variants = {"default": ({}, None)}
     for _ in range(a.rounds):
         for name, (cfg, lib) in variants.items():
             env = dict(os.environ)
