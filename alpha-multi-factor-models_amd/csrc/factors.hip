@@ -8,11 +8,12 @@
 //  * pandas' rolling/ewm kernels are sequential recurrences whose rounding depends on the full
 //    history (Kahan compensations are never reset), so bit-exactness requires a sequential scan
 //    per asset.  Parallelism = assets (one per lane) x indicator jobs (one job set per wave).
-//  * One workgroup = one 64-asset block: 15 job waves (balanced by the VALU count of each job's
-//    compiled step, and so that the four SIMDs carry equal totals) + 1 loader wave; the kernel
-//    is bound by f64 dependency latency at ~2.3 job waves per SIMD (~50 % VALU-busy, DESIGN.md
-//    §4).  An LDS ring holds the last kRing
-//    present observations of close and volume per lane.  A shard with few blocks (multi-GPU)
+//  * One 64-asset block = 15 job waves (balanced by the VALU count of each job's compiled step,
+//    and so that the four SIMDs carry equal totals) + a loader wave per item.  At config C the
+//    kernel is bound by its output stream in this pattern (~4.7 TB/s; without the stores it runs
+//    in ~2/3 of the time) beside the f64 VALU work; at small shards by the longest job set's
+//    dependency chain.  An LDS ring holds the last kRing present observations of
+//    close and volume per lane.  A shard with few blocks (multi-GPU)
 //    splits each block's 15 job waves over 3, 5 or 15 workgroups instead, so that ~all CUs work
 //    (each split needs its own ring; measured on MI355X, workgroups of 78 KB LDS do not
 //    co-reside -- the two-per-CU limit was between 52 and 56 KB -- hence one per CU).
@@ -192,8 +193,15 @@ struct Step {
     // global_store with an SGPR base (this day's column row) and the lane's 32-bit byte offset:
     // no per-store address arithmetic on the VALU
     __device__ __forceinline__ void store(int col, double x) {
+#ifdef AFM_FP_BUFSTORE            // experiment: buffer stores the scheduler may move and group
+        typedef unsigned v2u __attribute__((ext_vector_type(2)));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(out + col * plane), 0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, x), r, (int)voff, 0, 0);
+#else
         GLB double* base = out + col * plane;
         asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(x), "s"(base));
+#endif
     }
     __device__ __forceinline__ void put(int col, double x) {
         store(col, x);
@@ -1218,6 +1226,10 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                     rn.XY.fupd(st.r0 * st.g0);
                 }
                 jobs.fstep(st);
+#ifdef AFM_FP_STORE_LAST          // experiment: the step's arithmetic first, then its stores
+                __builtin_amdgcn_sched_group_barrier(0x0002, 1000, 0);
+                __builtin_amdgcn_sched_group_barrier(0x0200, 64, 0);
+#endif
                 n8 |= st.anynan ? 1u << s : 0u;
                 f8 |= st.anybad ? 1u << s : 0u;
                 ++p;
