@@ -14,8 +14,7 @@ struct afm_ctx {
     int magic = 0x61666d31;  // "afm1"
     // execution options (afm_ctx_set_option): work splits that must not change any result, set
     // by the invariance tests; 0 = the library's choice
-    int factor_split = 0;    // workgroups per 64-asset block of the factor kernel (a divisor of
-                             // the job-set count: 1, 3, 5, 15 or 3, 7, 21)
+    int factor_split = 0;    // workgroups per 64-asset block of the factor kernel (1, 3, 5, 15)
     int factor_pair = 1;     // 3-way split: two items per workgroup
     int factor_fast = 1;     // clean-window fast step on
     int gram_checked = 0;    // afm_xs_gram_f64: checked staging only (no FAST + REDO passes)

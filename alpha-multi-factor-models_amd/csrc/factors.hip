@@ -50,14 +50,10 @@ constexpr int kChunk = 8;
 // the loader fills chunk c+1 while the job waves scan chunk c: the ring must hold the scan's
 // lookback (57) plus two chunks
 constexpr int kRing = 57 + 2 * kChunk + 1;
-// job waves per 64-asset block (the partition W0.. below): 15 job sets, three items of 5 job
-// waves + a loader, two items per workgroup = 3 waves per SIMD at <= 168 VGPRs; or 21 job sets,
-// three items of 7 + a loader, 4 waves per SIMD at <= 128 VGPRs
-#ifndef AFM_FP_SETS
-#define AFM_FP_SETS 15
-#endif
-constexpr int kJobSets = AFM_FP_SETS;
-static_assert(kJobSets == 15 || kJobSets == 21, "job-set partitions: 15 or 21");
+// job waves per 64-asset block (the partition W0..W14 below): three items of 5 job waves + a
+// loader, two items per workgroup = 3 waves per SIMD at <= 168 VGPRs.  (A 21-set partition at
+// 4 waves per SIMD / 128 VGPRs measured no faster: DESIGN.md §4, round 3.)
+constexpr int kJobSets = 15;
 
 typedef unsigned long long u64;
 #ifdef AFM_FP_PROFILE
@@ -190,18 +186,16 @@ struct Step {
         return *(const LDS double*)((const LDS char*)&sm->v[0][0] + ring_off(pmoff, L));
     }
     __device__ __forceinline__ double div(double x, int n) const { return div_n(sm, x, n); }
-    // global_store with an SGPR base (this day's column row) and the lane's 32-bit byte offset:
-    // no per-store address arithmetic on the VALU
+    // buffer_store with an SGPR descriptor based at this day's column row and the lane's 32-bit
+    // byte offset: no per-store address arithmetic on the VALU, and (unlike an inline-asm store)
+    // the scheduler may place the store anywhere after its value (11.8-12.2 -> 11.2-11.4 ms at
+    // config C, bit-identical).  Raw buffer, stride 0: num_records bounds the byte offset
+    // (< lda * 8); word 3 = 0x00020000, the CDNA raw-buffer format word.
     __device__ __forceinline__ void store(int col, double x) {
-#ifdef AFM_FP_BUFSTORE            // experiment: buffer stores the scheduler may move and group
         typedef unsigned v2u __attribute__((ext_vector_type(2)));
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(out + col * plane), 0, 0x7fffffff, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, x), r, (int)voff, 0, 0);
-#else
-        GLB double* base = out + col * plane;
-        asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(x), "s"(base));
-#endif
     }
     __device__ __forceinline__ void put(int col, double x) {
         store(col, x);
@@ -995,7 +989,6 @@ struct Pack<H, R...> {
     }
 };
 
-#if AFM_FP_SETS == 15
 // Static job partition over the 15 job waves of one workgroup (LPT on the per-job VALU count of
 // the compiled step: Corr ~550, RetSd5x15 ~360, VolSd5x15 ~290, BB ~220, VWMA ~170, RetSd3 /
 // VolSd3 / PvtObvPsy ~155, RSI ~115, SMA / MomAccelRocr ~100, MACD ~75, EMA ~60; ~620 per wave),
@@ -1021,37 +1014,6 @@ using W13 = Pack<Bbands<20>, Vwma<34>, MomAccelRocr<38>, Sma<46>, Sma<6>>;
 using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>, Ema<6>>;
 #define AFM_FP_FOR_SETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
     X(13) X(14)
-#else
-// 21 job sets: each rolling correlation alone on a wave, the other jobs grouped so that a set's
-// windows share lookbacks; per item type (7 sets) the waves at positions p and p + 4 share a
-// SIMD in both halves of the pair, so positions (0, 4), (1, 5), (2, 6) carry about the work of
-// position 3 (the heaviest set, beside the loader at position 7).  Fast-step VALU per job:
-// Corr ~260, RetSd5x15 ~190, VolSd5x15 ~140, RetSd3 ~100, Bbands ~80, Vwma ~65, VolSd3 ~65,
-// PvtObvPsy ~60, Rsi ~55, MomAccelRocr ~35, Sma ~25, Macd ~15, Ema ~8.
-using W0 = Pack<Bbands<14>, MomAccelRocr<14>, Sma<14>, Ema<14>>;
-using W1 = Pack<Bbands<20>, MomAccelRocr<20>, Sma<18>, Ema<18>>;
-using W2 = Pack<Bbands<26>, MomAccelRocr<26>, Sma<26>, Ema<26>>;
-using W3 = Pack<Corr<5, true>>;
-using W4 = Pack<Rsi<8>, Rsi<14>, Macd<30>>;
-using W5 = Pack<Vwma<10>, Vwma<18>, Ema<22>>;
-using W6 = Pack<Vwma<22>, Vwma<26>, Ema<34>>;
-using W7 = Pack<Bbands<32>, MomAccelRocr<32>, Sma<30>, Ema<30>>;
-using W8 = Pack<Bbands<38>, MomAccelRocr<38>, Sma<38>, Ema<38>>;
-using W9 = Pack<Bbands<44>, MomAccelRocr<44>, Sma<42>, Ema<42>>;
-using W10 = Pack<Corr<15, false>>;
-using W11 = Pack<Rsi<20>, Vwma<14>>;
-using W12 = Pack<Vwma<30>, Vwma<34>, Sma<34>>;
-using W13 = Pack<Vwma<38>, Vwma<42>, Sma<22>>;
-using W14 = Pack<Bbands<50>, MomAccelRocr<50>, Sma<50>, Ema<50>>;
-using W15 = Pack<Bbands<56>, MomAccelRocr<56>, Sma<46>, Ema<46>>;
-using W16 = Pack<RetSd3, Sma<6>, Ema<10>, Macd<18>>;
-using W17 = Pack<RetSd5x15, VolSd3>;
-using W18 = Pack<Vwma<46>, Vwma<50>, Macd<24>>;
-using W19 = Pack<VolSd5x15, Ema<6>>;
-using W20 = Pack<PvtObvPsy, Vwma<6>, Sma<10>>;
-#define AFM_FP_FOR_SETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
-    X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)
-#endif
 
 // The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
 // job waves (one per chunk).  It also publishes, per lane and
@@ -1226,10 +1188,6 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                     rn.XY.fupd(st.r0 * st.g0);
                 }
                 jobs.fstep(st);
-#ifdef AFM_FP_STORE_LAST          // experiment: the step's arithmetic first, then its stores
-                __builtin_amdgcn_sched_group_barrier(0x0002, 1000, 0);
-                __builtin_amdgcn_sched_group_barrier(0x0200, 64, 0);
-#endif
                 n8 |= st.anynan ? 1u << s : 0u;
                 f8 |= st.anybad ? 1u << s : 0u;
                 ++p;
@@ -1326,11 +1284,15 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
         nb |= (u64)n8 << sh;
         fb |= (u64)f8 << sh;
         if (sh + kChunk == 64 || ch + 1 == nch) {          // word end: this wave's partial words
-            // SGPR row base + lane offset, as the output stores (a compiler-visible store here
-            // would make it drain the wave's output stores before reusing the registers)
+            // SGPR row base + lane offset, as the output stores
             const int64_t wrow = (((int64_t)(ch * kChunk) >> 6) - w0) * a.lda;
-            asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(nb), "s"(a.nanpart + wrow));
-            asm volatile("global_store_dwordx2 %0, %1, %2" ::"v"(voff), "v"(fb), "s"(a.badpart + wrow));
+            typedef unsigned v2u __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, nb),
+                __builtin_amdgcn_make_buffer_rsrc((void*)(a.nanpart + wrow), 0, 0x7fffffff,
+                                                  0x00020000), (int)voff, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, fb),
+                __builtin_amdgcn_make_buffer_rsrc((void*)(a.badpart + wrow), 0, 0x7fffffff,
+                                                  0x00020000), (int)voff, 0, 0);
             nb = 0ull;
             fb = 0ull;
         }
@@ -1417,20 +1379,11 @@ constexpr int kStateWords = AFM_FP_FOR_SETS(AFM_FP_STATE_WORDS) 2 * kRing + 3
 // Wave w of a workgroup issues on SIMD w % 4; the layouts minimise the busiest SIMD's measured
 // cycles (tools/wave_profile.py; type 1: 61.3 -> 55.0 Mcycles; round 2 re-checked for the new
 // partition with AFM_FP_LAYOUT, tools/gpu_layout.sh: four other layouts per type, none faster).
-#if AFM_FP_SETS == 15
 __constant__ signed char kPairLayout[3][2][6] = {
     {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
     {{0, 2, 3, 4, 1, 5}, {1, 2, 3, 4, 0, 5}},
     {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
 };
-#else
-// the partition above is ordered by position already (loader at position 7)
-__constant__ signed char kPairLayout[3][2][8] = {
-    {{0, 1, 2, 3, 4, 5, 6, 7}, {0, 1, 2, 3, 4, 5, 6, 7}},
-    {{0, 1, 2, 3, 4, 5, 6, 7}, {0, 1, 2, 3, 4, 5, 6, 7}},
-    {{0, 1, 2, 3, 4, 5, 6, 7}, {0, 1, 2, 3, 4, 5, 6, 7}},
-};
-#endif
 // waves per SIMD a launch shape needs resident (the VGPR budget): the paired 3-way launch fills
 // the CU's four SIMDs evenly; the other splits allow 2 (256 VGPRs)
 template <int TYPES, bool PAIR>
@@ -1601,11 +1554,7 @@ static int factor_types(afm_ctx* ctx, int64_t nblk) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
         ncu = 256;
     int types = 3;
-#if AFM_FP_SETS == 15
     for (int t : {5, 15})
-#else
-    for (int t : {7, 21})
-#endif
         if (nblk * t <= 2 * (int64_t)ncu) types = t;
     if (ctx->factor_split) types = ctx->factor_split;              // option factor_split
     return types;
@@ -1676,9 +1625,7 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
         case 3: rc = pair ? launch_split<3, true>(ctx, nblk, a) : launch_split<3, false>(ctx, nblk, a);
                 break;
         case 5: rc = launch_split<5, false>(ctx, nblk, a); break;
-        case 7: rc = launch_split<7, false>(ctx, nblk, a); break;
         case 15: rc = launch_split<15, false>(ctx, nblk, a); break;
-        case 21: rc = launch_split<21, false>(ctx, nblk, a); break;
         default:
             afm_set_error("factor kernel: factor_split is not a split of the job sets");
             rc = AFM_E_ARG;
