@@ -30,21 +30,25 @@ __device__ __forceinline__ double bcast(double v, int lane) {
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), lane);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-// value of feature j from the (v0: j < 64, v1: j >= 64) register pair, j uniform
+// value of feature j from the (v0: j < 64, v1: j >= 64) register pair, j uniform: both lanes
+// read, then a scalar select (no branch on the coordinate's half)
 __device__ __forceinline__ double pick(double v0, double v1, int j) {
-    return j < 64 ? bcast(v0, j) : bcast(v1, j - 64);
+    const double a = bcast(v0, j & 63), b = bcast(v1, j & 63);
+    return j < 64 ? a : b;
 }
 __device__ __forceinline__ double fsign(double f) { return f == 0.0 ? 0.0 : (f > 0.0 ? 1.0 : -1.0); }
 // x / d with r = RN(1 / d): Markstein's correction q0 = RN(x r), e = fma(-q0, d, x),
 // q = RN(q0 + e r) is the IEEE quotient when r is the correctly rounded reciprocal and nothing
-// under- or overflows (checked on 5.6e8 hard and random cases, tools/markstein_any.c); zero,
-// non-finite and tiny quotients take the IEEE division.
+// under- or overflows (checked on 5.6e8 hard and random cases, tools/markstein_any.c).  A zero x
+// gives x itself (d > 0: the signed zero the division would give); a quotient outside
+// [2^-400, 2^400] takes the IEEE division (a uniform branch, never in practice).
 __device__ __forceinline__ double div_r(double x, double d, double r) {
     const double q0 = x * r;
     const double e = __builtin_fma(-q0, d, x);
     const double q1 = __builtin_fma(e, r, q0);
     const double aq = __builtin_fabs(q0);
-    return (aq > 0x1p-400 && aq < 0x1p400) ? q1 : x / d;
+    if (__builtin_expect(!(aq > 0x1p-400 && aq < 0x1p400), 0)) return x == 0.0 ? x : x / d;
+    return q1;
 }
 
 // alpha_row >= 0: alpha = alpha_row * n (sklearn's alpha times the row count, read on the device);
@@ -92,6 +96,7 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     double rd0 = 1.0 / dd0, rd1 = 1.0 / dd1;
     if (!(__builtin_fabs(rd0) > 0x1p-400 && __builtin_fabs(rd0) < 0x1p400)) rd0 = 0.0;
     if (!(__builtin_fabs(rd1) > 0x1p-400 && __builtin_fabs(rd1) < 0x1p400)) rd1 = 0.0;
+    const bool all_rd = __ballot((has0 && rd0 == 0.0) || (has1 && rd1 == 0.0)) == 0ull;
     auto movable = [&](double qd, double q, double h, double w) {
         const double tmp = q - h;
         const bool nz = (positive && tmp < 0) ? false : __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0) != 0.0;
@@ -116,37 +121,40 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
                     if (ii >= p) break;
                 }
             }
+            // (the ballot above never stops at a coordinate with a zero diagonal: not movable)
             const double* row = Q + ii * p;
-            const double qii = pick(qd0, qd1, ii);
-            if (qii == 0.0) continue;
             const double r0 = has0 ? row[j0] : 0.0, r1 = has1 ? row[j1] : 0.0;
+            const double qii = pick(qd0, qd1, ii);
             const double w_ii = pick(w0, w1, ii);
             // H[ii] after the first axpy is lane ii's own fma (r = Q[ii][ii] there): computed on
             // the scalar path directly, so the step does not wait for the row read or the axpy
             const double h_ii = pick(h0, h1, ii);
             const double hh = w_ii != 0.0 ? __builtin_fma(-w_ii, qii, h_ii) : h_ii;
-            if (w_ii != 0.0) {
-                h0 = __builtin_fma(-w_ii, r0, h0);
-                h1 = __builtin_fma(-w_ii, r1, h1);
-            }
+            // the axpys run unconditionally: with a zero weight fma(+-0, r, h) = h for the finite
+            // Gram (a zero h may change the sign of its zero, which reaches no weight: h enters
+            // only through q - h and further fmas)
+            h0 = __builtin_fma(-w_ii, r0, h0);
+            h1 = __builtin_fma(-w_ii, r1, h1);
             const double tmp = pick(q0, q1, ii) - hh;
             double wn;
             if (positive && tmp < 0) {
                 wn = 0.0;
             } else {
                 const double num = fsign(tmp) * __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0);
-                const double rdi = pick(rd0, rd1, ii);
-                wn = rdi != 0.0 ? div_r(num, qii + beta, rdi) : num / (qii + beta);
+                if (all_rd) {
+                    wn = div_r(num, qii + beta, pick(rd0, rd1, ii));
+                } else {
+                    const double rdi = pick(rd0, rd1, ii);
+                    wn = rdi != 0.0 ? div_r(num, qii + beta, rdi) : num / (qii + beta);
+                }
             }
-            if (ii < 64) { if (lane == ii) w0 = wn; }
-            else if (lane == ii - 64) w1 = wn;
-            if (wn != 0.0) {
-                h0 = __builtin_fma(wn, r0, h0);
-                h1 = __builtin_fma(wn, r1, h1);
-            }
-            const double d_w_ii = __builtin_fabs(wn - w_ii);
-            if (d_w_ii > d_w_max) d_w_max = d_w_ii;
-            if (__builtin_fabs(wn) > w_max) w_max = __builtin_fabs(wn);
+            w0 = lane == ii ? wn : w0;
+            w1 = lane + 64 == ii ? wn : w1;
+            h0 = __builtin_fma(wn, r0, h0);
+            h1 = __builtin_fma(wn, r1, h1);
+            // NaN-free: fmax keeps the larger, as the comparisons did
+            d_w_max = __builtin_fmax(__builtin_fabs(wn - w_ii), d_w_max);
+            w_max = __builtin_fmax(__builtin_fabs(wn), w_max);
         }
         if (w_max == 0.0 || d_w_max / w_max < d_w_tol || n_iter == max_iter - 1) {
             double q_dot_w = 0.0, wh = 0.0, w_norm2 = 0.0, asum = 0.0, dual = 0.0;
