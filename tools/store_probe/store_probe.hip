@@ -14,7 +14,7 @@
 constexpr int kChunk = 8, kPlanes = 96;
 
 __global__ __launch_bounds__(768) void probe(double* out, const double* in, long T, long lda,
-                                             int nblk, int mode, long pad, int G) {
+                                             int nblk, int mode, long pad, int G, int work) {
     const int lane = threadIdx.x & 63, wall = threadIdx.x >> 6;
     const int half = wall >= 6 ? 1 : 0, pos = wall - 6 * half;
     const long item = 2L * blockIdx.x + half;
@@ -51,7 +51,14 @@ __global__ __launch_bounds__(768) void probe(double* out, const double* in, long
                     if (t >= T) break;
                     const long off = (mode & 8) ? c * plane + block * (T * 64) + t * 64 + lane
                                                 : c * plane + t * lda + asset;
-                    out[off] = (double)t + c;
+                    // `work` f64 FMAs on 4 independent chains per stored value (compute beside
+                    // the stores, as in the factor kernel)
+                    double v0 = (double)t + c, v1 = v0 + 1, v2 = v0 + 2, v3 = v0 + 3;
+                    for (int w = 0; w < work; w += 4) {
+                        v0 = __builtin_fma(v0, 1.0000001, 0.5); v1 = __builtin_fma(v1, 1.0000001, 0.5);
+                        v2 = __builtin_fma(v2, 1.0000001, 0.5); v3 = __builtin_fma(v3, 1.0000001, 0.5);
+                    }
+                    out[off] = v0 + v1 + v2 + v3;
                 }
             }
         } else if (live && pos < 5 && (mode & 3) != 2) {
@@ -98,6 +105,7 @@ int main(int argc, char** argv) {
     const int mode = argc > 3 ? atoi(argv[3]) : 0;
     const long pad = argc > 4 ? atol(argv[4]) : 0;
     const int G = argc > 5 ? atoi(argv[5]) : kChunk;
+    const int work = argc > 6 ? atoi(argv[6]) : 0;      // f64 FMAs per stored value (mode 32)
     const long lda = (A + 63) / 64 * 64;
     const int nblk = (int)(lda / 64);
     double *out, *in;
@@ -118,13 +126,13 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL(stream, dim3(4096), dim3(256), 0, 0, (dv2*)out,
                                (long)kPlanes * T * lda / 2, mode & 1);
         else
-            hipLaunchKernelGGL(probe, dim3(grid), dim3(768), 0, 0, out, in, T, lda, nblk, mode, pad, G);
+            hipLaunchKernelGGL(probe, dim3(grid), dim3(768), 0, 0, out, in, T, lda, nblk, mode, pad, G, work);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms = 0;
         hipEventElapsedTime(&ms, e0, e1);
         const double gb = ((mode & 3) == 2 ? 16.0 : 8.0 * kPlanes) * T * A / 1e9;
-        printf("mode %d G %d T %ld A %ld pad %ld: %.3f ms  %.2f GB  %.2f TB/s\n", mode, G, T, A, pad, ms, gb,
+        printf("work %d mode %d G %d T %ld A %ld pad %ld: %.3f ms  %.2f GB  %.2f TB/s\n", work, mode, G, T, A, pad, ms, gb,
                gb / ms);
     }
     return 0;
