@@ -43,7 +43,6 @@ All buffers are allocated once; a step does no host synchronisation.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -100,6 +99,14 @@ class PipelineConfig:
     # variant may name another subset -- e.g. DENSE_FEATURES, which drops tmr_ret1d (the
     # undemeaned twin of the target, NT:90-91) so the Lasso keeps many coefficients
     features: tuple | None = None
+    # stream placement (moves work between streams only; the outputs are bitwise the same):
+    # labels_side -- one GPU: the two label planes on a side stream beside the factor kernel;
+    # fm_fork -- one GPU: where the FM per-date Grams fork off the main stream ("gram", "predict",
+    # "analyzer" or "rebalance"; measured best: "predict"); main_priority -- the main stream at
+    # high priority
+    labels_side: bool = True
+    fm_fork: str = "predict"
+    main_priority: bool = True
 
 
 @dataclass
@@ -340,8 +347,10 @@ class Pipeline:
                 "ir_scratch": torch.empty((3 * self.an_nyears, nad), **f64),
             })
         self.ctx = _lib.Context.get(dev.index)
-        prio = os.environ.get("AFM_PIPE_PRIO", "1") != "0"
-        self.main = torch.cuda.Stream(device=dev, priority=-8 if prio else 0)
+        if c.fm_fork not in ("gram", "predict", "analyzer", "rebalance"):
+            raise ValueError(f"fm_fork={c.fm_fork!r}: expected gram, predict, analyzer or "
+                             "rebalance")
+        self.main = torch.cuda.Stream(device=dev, priority=-8 if c.main_priority else 0)
         self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
         self.labels_done = torch.cuda.Event()
@@ -427,7 +436,7 @@ class Pipeline:
             mark("factors", 0)
             # one GPU: the two label planes on the side stream, enqueued after the factor kernel
             # (it runs on the CUs the factor workgroups leave free); zstats waits for them
-            lab_side = W == 1 and os.environ.get("AFM_LABELS_SIDE", "1") != "0"
+            lab_side = W == 1 and c.labels_side
             if self.A_r > 0:
                 chk(L.afm_factors_f64(h, T, self.A_r, lda_r, P(g.close), P(g.volume),
                                       None if lab_side else P(g.ret1d),
@@ -506,10 +515,7 @@ class Pipeline:
                     mark("fm", 1)
                 return self.ctx.bind_stream()
 
-            fm_at = os.environ.get("AFM_FM_FORK", "predict") if W == 1 else "gram"
-            if fm_at not in ("gram", "predict", "analyzer", "rebalance"):
-                raise ValueError(f"AFM_FM_FORK={fm_at!r}: expected gram, predict, analyzer or "
-                                 "rebalance")
+            fm_at = c.fm_fork if W == 1 else "gram"
             if fm_at == "gram":
                 h = fork_fm()
             mark("lasso", 0)

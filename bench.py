@@ -260,7 +260,7 @@ def main():
         # (HBM: 816 B per asset-day; 784 B without the two label planes, which
         # run on a side stream beside the factor kernel) and the pooled Gram (fp64 MFMA:
         # rows * (p+2)(p+3) flops over the train + valid rows, zpool + tree merges).
-        labels_in = world == 1 and os.environ.get("AFM_LABELS_SIDE", "1") == "0"
+        labels_in = world == 1 and not pipe.cfg.labels_side
         fac_bytes = FACTOR_BYTES_PER_AD if labels_in else FACTOR_BYTES_NO_LABELS
         fac_gbs = fac_bytes * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
         rows_tv = float(pipe.pool_g[0, 0, 0].item())           # pooled rows (n of the Gram)

@@ -129,17 +129,16 @@ def test_fama_macbeth_vs_golden(chain_a):
     assert err.max() < 1e-9, err.max()
 
 
-@pytest.mark.parametrize("env", [("AFM_LABELS_SIDE", "0"), ("AFM_FM_FORK", "gram"),
-                                 ("AFM_FM_FORK", "rebalance")])
-def test_stream_placement_bit_identical(chain_a, env, monkeypatch):
+@pytest.mark.parametrize("place", [{"labels_side": False}, {"fm_fork": "gram"},
+                                   {"fm_fork": "rebalance"}])
+def test_stream_placement_bit_identical(chain_a, place):
     """The side-stream placements (label planes beside the factor kernel, the FM fork point) move
     work between streams only: the step's outputs are bitwise those of the default placement."""
     import torch
     from afm.pipeline import Pipeline, PipelineConfig
     p, pipe, gold, C = chain_a
-    monkeypatch.setenv(*env)
     other = Pipeline(pipe.g, PipelineConfig(train_end=C["train_end"], valid_end=C["valid_end"],
-                                            window=C["window"], top_n=C["top_n"]))
+                                            window=C["window"], top_n=C["top_n"], **place))
     other.step()
     torch.cuda.synchronize()
     for name in ("out", "pred", "lasso_beta", "fm_beta"):
