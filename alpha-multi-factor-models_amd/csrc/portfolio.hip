@@ -104,6 +104,16 @@ __device__ __forceinline__ int tri(int a, int b) {
 // factor of the QP or the tie buffer of the selection.  The factor is packed by member PAIR: the
 // entry of {q, q'} belongs to whichever of the two was factored later (row) -- one orientation
 // per pair -- so members can leave and join the factor order without moving data.
+// LDS of the workgroup QP (qp_block): broadcast vectors, the two column halves' partial
+// products and the reduction slots
+struct QpLds {
+    double pub[2][128];                  // a published row of M (double-buffered in the sweep)
+    double vc[128], vw[128], vu[128];    // broadcast vectors: S_FB w_B, w, u~
+    double part[4][2][128];              // [product][column half][row]
+    double red[6][4][4];                 // [use][wave][value]
+    int code[4];
+};
+
 template <int KM>
 struct Shared {
     u64 pw[3][kMaxWords];                // prediction presence rows: prev, cur, next
@@ -117,9 +127,11 @@ struct Shared {
     double w[KM], x[KM], c[KM];
     double sinv[258];                    // 1 / n for the Welford updates (n <= 257)
     double S[KM * (KM + 1) / 2];
+    u64 pm[KM];                          // presence words of the staged chunk (MFMA covariance)
     union {
         double hv[KM][65];               // staged history chunk [member][date]
         double L[KM * (KM + 1) / 2];     // Cholesky factor of S_FF (packed by member pair)
+        QpLds qp;                        // the workgroup QP of books of more than 32 names
     } u;
 };
 
@@ -209,14 +221,14 @@ __device__ __forceinline__ void book_cov(Shared<KM>& sh, const int k, const int6
 // ---- pairwise-complete covariance on fp64 MFMA (books of more than 32 names) -----------------
 // The same statistic as book_cov (pandas nancorr(cov=True): per pair, the rows where both values
 // are finite) written as masked SYRKs over the window.  With m the presence mask, c_m a centring
-// constant per member (the mean of its finite values) and x~ = m * (x - c_m):
+// constant per member and x~ = m * (x - c_m):
 //   N = M M',  C = X~ X~',  P = X~ M',  Q = M X~'     (P_ij = sum over both-present rows of x~_i,
 //   Q_ij = the same of x~_j), cov_ij = (C_ij - P_ij Q_ij / N_ij) / (N_ij - 1), NaN for N_ij < 2.
-// Every product is v_mfma_f64_16x16x4_f64 on 16-member tiles (the window rows are the k dim):
-// 36 tile pairs (I <= J) of at most 8 tiles, pair q on wave q % 4.  Pass 0 stages the window
-// once for the member means and N (written into S), pass 1 again for C, P, Q (27 accumulators
-// per wave), then each element is finished in place.  Work: 2 * rows * k^2 flop per product.
-// Centring keeps P and Q small, so the difference C - PQ/N does not cancel (rel ~1e-15 of S on
+// C, P and Q are v_mfma_f64_16x16x4_f64 on 16-member tiles (the window rows are the k dim): 36
+// tile pairs (I <= J) of at most 8 tiles, pair q on wave q % 4, 27 accumulators per wave, ONE pass
+// over the window; N is counted on the VALU from the staged chunk's presence words (popcount of
+// m_i & m_j per 64 rows).  c_m is the member's first finite value in the window's first 64 rows
+// (shifted data: the cancellation in C - PQ/N is then O(1) in the variance, rel ~1e-15 of S on
 // the test books, vs 1e-12 for the bar of tests/test_portfolio_gpu.py).
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -229,7 +241,8 @@ struct CovPairs {
     }
 };
 
-// stage rows [h0, h0 + 64) of the k members into sh.u.hv (NaN past the window)
+// stage rows [h0, h0 + 64) of the k members into sh.u.hv (NaN past the window), with each
+// member's presence word (bit d: row h0 + d finite) in sh.pm
 template <int KM, class Get>
 __device__ __forceinline__ void cov_stage(Shared<KM>& sh, const int k, const int64_t h0, Get get) {
     constexpr int EPT = KM * 64 / kT;
@@ -243,43 +256,58 @@ __device__ __forceinline__ void cov_stage(Shared<KM>& sh, const int k, const int
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-        const int e = tid + j * kT;
+        const int e = tid + j * kT;                  // member e >> 6 (uniform per wave), row lane
+        const u64 m = __ballot(e < k * 64 && __builtin_isfinite(v[j]));
         if (e < k * 64) sh.u.hv[e >> 6][e & 63] = v[j];
+        if ((tid & 63) == 0 && e < k * 64) sh.pm[e >> 6] = m;
     }
     __syncthreads();
 }
 
-// pass 0 (S0 < 0): the member means (thread per member, into sh.x) and N (into S).
-// pass 1 (slots [S0, S0 + NS) of this wave): C, P, Q, then those elements finished in place.
-template <int KM, int W, int S0, int NS, class Get>
-__device__ void cov_mfma_pass(Shared<KM>& sh, const int k, const int64_t rows, Get get) {
+template <int KM, int W, class Get>
+__device__ __noinline__ void cov_mfma_wave(Shared<KM>& sh, const int k, const int64_t rows,
+                                           Get get) {
     static_assert(KM == 128, "MFMA covariance: 8 tiles of 16 members");
     constexpr CovPairs tab{};
-    constexpr bool P0 = S0 < 0;
-    constexpr int SB = P0 ? 0 : S0;
+    constexpr int NS = 9;                            // slots: pair q = W + 4 s
     const int tid = threadIdx.x, lane = tid & 63;
     const int fi = lane & 15, kk = lane >> 4;
     const int nt = (k + 15) / 16;
     double mu[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) mu[t] = !P0 && 16 * t + fi < k ? sh.x[16 * t + fi] : 0.0;
     d4 c[NS], pp[NS], qq[NS];
+    int nn[NS][4];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         c[s] = d4{0.0, 0.0, 0.0, 0.0};
         pp[s] = c[s];
         qq[s] = c[s];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) nn[s][r] = 0;
     }
-    double msum = 0.0;
-    int mcnt = 0;
     for (int64_t h0 = 0; h0 < rows; h0 += 64) {
         cov_stage(sh, k, h0, get);
-        if (P0 && tid < k) {
-            for (int d = 0; d < 64; ++d) {
-                const double v = sh.u.hv[tid][d];
-                const bool f = h0 + d < rows && __builtin_isfinite(v);
-                msum += f ? v : 0.0;
-                mcnt += f ? 1 : 0;
+        if (h0 == 0) {                               // centring constants
+            if (tid < k) {
+                double c0 = 0.0;
+                for (int d = 0; d < 64; ++d) {
+                    const double v = sh.u.hv[tid][d];
+                    if (__builtin_isfinite(v)) { c0 = v; break; }
+                }
+                sh.x[tid] = c0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int t = 0; t < 8; ++t) mu[t] = 16 * t + fi < k ? sh.x[16 * t + fi] : 0.0;
+        }
+        // N: both-present counts of this chunk's rows, element (16 I + kk + 4 r, 16 J + fi)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int q = W + 4 * s;
+            if (q < 36 && tab.J[q] < nt) {
+                const u64 mj = sh.pm[16 * tab.J[q] + fi];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    nn[s][r] += __popcll(mj & sh.pm[16 * tab.I[q] + kk + 4 * r]);
             }
         }
         const int nks = (int)((rows - h0) < 64 ? (rows - h0 + 3) / 4 : 16);
@@ -295,50 +323,33 @@ __device__ void cov_mfma_pass(Shared<KM>& sh, const int k, const int64_t rows, G
             }
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-                const int q = W + 4 * (SB + s);
+                const int q = W + 4 * s;
                 if (q < 36 && tab.J[q] < nt) {
                     const int I = tab.I[q], J = tab.J[q];
-                    if (P0) {
-                        c[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(m[I], m[J], c[s], 0, 0, 0);
-                    } else {
-                        c[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I], x[J], c[s], 0, 0, 0);
-                        pp[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I], m[J], pp[s], 0, 0, 0);
-                        qq[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(m[I], x[J], qq[s], 0, 0, 0);
-                    }
+                    c[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I], x[J], c[s], 0, 0, 0);
+                    pp[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I], m[J], pp[s], 0, 0, 0);
+                    qq[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(m[I], x[J], qq[s], 0, 0, 0);
                 }
             }
         }
     }
-    if (P0 && tid < k) sh.x[tid] = mcnt ? msum / (double)mcnt : 0.0;   // centring constants
-    // element (i, j), i >= j (one lane each): pass 0 stores N, pass 1 replaces it by the cov
+    // element (i, j), i >= j (one lane each)
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-        const int q = W + 4 * (SB + s);
+        const int q = W + 4 * s;
         if (q < 36 && tab.J[q] < nt) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 16 * tab.I[q] + kk + 4 * r, j = 16 * tab.J[q] + fi;
                 if (i < k && j < k && (tab.I[q] < tab.J[q] || i >= j)) {
-                    if (P0) {
-                        sh.S[tri(i, j)] = c[s][r];
-                    } else {
-                        const double nn = sh.S[tri(i, j)];
-                        sh.S[tri(i, j)] = nn >= 2.0 ? (c[s][r] - pp[s][r] * qq[s][r] / nn) /
-                                                          (nn - 1.0)
+                    const double n = (double)nn[s][r];
+                    sh.S[tri(i, j)] = nn[s][r] >= 2 ? (c[s][r] - pp[s][r] * qq[s][r] / n) /
+                                                          (n - 1.0)
                                                     : __builtin_nan("");
-                    }
                 }
             }
         }
     }
-    __syncthreads();
-}
-
-template <int KM, int W, class Get>
-__device__ void cov_mfma_wave(Shared<KM>& sh, const int k, const int64_t rows, Get get) {
-    cov_mfma_pass<KM, W, -1, 9>(sh, k, rows, get);    // means + N
-    cov_mfma_pass<KM, W, 0, 5>(sh, k, rows, get);     // C, P, Q of slots 0..4
-    cov_mfma_pass<KM, W, 5, 4>(sh, k, rows, get);     // slots 5..8
 }
 
 template <int KM, class Get>
@@ -900,6 +911,268 @@ __device__ __forceinline__ bool qp_wave(Shared<KM>& sh, const int n, const doubl
 }
 
 
+// ---- the QP of books of more than 32 names, on the whole workgroup ------------------------------
+// The method, start point and pivot rules of qp_setup + qp_wave, laid out for 256 threads: thread
+// t owns member row a = t & 127 and column half h = t >> 7 (columns 64h .. 64h + 63) of
+// M = S_FF^-1 in REGISTERS, M embedded in the full 128 x 128 index space with the rows and columns
+// of bound members and non-members exactly zero; S stays packed in LDS.  The bound set (and which
+// bound) is tracked as uniform bit masks, so S_FB w_B, the bound weight sum and the multipliers
+// need no gather.  Every product with M is a register mat-vec against a vector broadcast from
+// LDS (the two halves' partials summed through LDS), and the active-set changes move no data:
+//   join j (bordering):  u = M s (s = S[.][j]), d = S_jj - s'u, M <- M + u~ u~' / d with
+//                        u~ = u - e_j (u_j = 0: row j of M is zero);
+//   leave j (deflation): M <- M - m m' / m_jj (m = M[.][j]), then row and column j set to 0.
+// Every update is one FMA per element with the row factor (x_a r) precomputed; M is symmetric to
+// rounding, so a published ROW serves as the column (the optimum is unique: only the end point is
+// compared, rel 1e-9).  The sweep operator builds M = S^-1 in the same layout, one published row
+// per pivot.  Returns true if the iteration cap was hit (or S is not finite: weights NaN).
+__device__ __forceinline__ void blk_sum3(double (&red)[4][4], double& x, double& y, double& z) {
+    x = wave_sum(x);
+    y = wave_sum(y);
+    z = wave_sum(z);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[wv][0] = x;
+        red[wv][1] = y;
+        red[wv][2] = z;
+    }
+    __syncthreads();
+    x = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+    y = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
+    z = ((red[0][2] + red[1][2]) + red[2][2]) + red[3][2];
+}
+
+// lexicographic (v, code) minimum over the workgroup, in every thread
+__device__ __forceinline__ void blk_argmin(QpLds& q, double& v, int& code) {
+    wave_argmin(v, code);
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        q.red[5][wv][0] = v;
+        q.code[wv] = code;
+    }
+    __syncthreads();
+    v = q.red[5][0][0];
+    code = q.code[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+        const double v2 = q.red[5][w][0];
+        const int c2 = q.code[w];
+        if (v2 < v || (v2 == v && c2 < code)) { v = v2; code = c2; }
+    }
+}
+
+__device__ __forceinline__ bool mbit(const u64 (&m)[2], int b) {
+    return (m[b >> 6] >> (b & 63)) & 1ull;
+}
+
+template <int KM>
+__device__ __noinline__ bool qp_block(Shared<KM>& sh, const int n, const double lo,
+                                     const double hi, int64_t* stamps) {
+    static_assert(KM == 128 && kT == 256, "qp_block: 128 member rows x 2 column halves");
+    QpLds& q = sh.u.qp;
+    const int tid = threadIdx.x, a = tid & 127, h = tid >> 7, b0 = 64 * h;
+    const int wv = tid >> 6, lane = tid & 63;
+    const bool mem = a < n;
+    double Mr[64];
+    int bad = 0;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        const int b = b0 + i;
+        Mr[i] = mem && b < n ? sh.S[tri(a, b)] : 0.0;
+        bad |= !__builtin_isfinite(Mr[i]);
+    }
+    if (__syncthreads_or(bad)) {
+        if (h == 0 && mem) sh.w[a] = __builtin_nan("");
+        __syncthreads();
+        return true;
+    }
+    // sweep(k): A_ab -= A_ak A_kb / A_kk (a, b != k); A_ak /= A_kk; A_kk = -1 / A_kk -> A = -S^-1
+    for (int k = 0; k < n; ++k) {
+        double* pub = q.pub[k & 1];
+        if (a == k) {                                  // publish row k, then drop it
+#pragma unroll
+            for (int i = 0; i < 64; ++i) pub[b0 + i] = Mr[i];
+#pragma unroll
+            for (int i = 0; i < 64; ++i) Mr[i] = 0.0;
+        }
+        __syncthreads();
+        // one FMA per element: row k (zeroed, pa = -1) becomes A_kb / A_kk; column k is set to
+        // pa / A_kk (-1 / A_kk on the diagonal) in the one 16-column chunk that holds it
+        const double rd = 1.0 / pub[k];
+        const double prd = (a == k ? -1.0 : pub[a]) * rd;
+#pragma unroll
+        for (int i0 = 0; i0 < 64; i0 += 16) {
+            double pb[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) pb[i] = pub[b0 + i0 + i];
+            if (k >= b0 + i0 && k < b0 + i0 + 16) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    Mr[i0 + i] = b0 + i0 + i == k ? prd : __builtin_fma(-pb[i], prd, Mr[i0 + i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) Mr[i0 + i] = __builtin_fma(-pb[i], prd, Mr[i0 + i]);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) Mr[i] = -Mr[i];
+    if (stamps && tid == 0) stamps[6] = wall_clock64();
+
+    u64 bnd[2] = {0ull, 0ull}, bhi[2] = {0ull, 0ull};   // uniform: bound members, those at hi
+    double wa = mem ? 1.0 / n : 0.0;                    // own member's weight
+    int nf = n;
+    bool capped = false;
+    const int max_it = 4 * n + 8;
+    int it = 0;
+    for (; it < max_it; ++it) {
+        if (nf == 0) break;
+        if (it == max_it - 1) capped = true;
+        const bool ba = mem && mbit(bnd, a), fa = mem && !ba;
+        // c = S_FB w_B and the bound weight sum, bound members in ascending order
+        double ca = 0.0, bs = 0.0;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            u64 m = bnd[r];
+            while (m) {
+                const int b = 64 * r + __builtin_ctzll(m);
+                m &= m - 1ull;
+                const double wb = mbit(bhi, b) ? hi : lo;
+                bs += wb;
+                if (h == 0) ca = ca + sh.S[tri(a, b)] * wb;
+            }
+        }
+        if (h == 0) q.vc[a] = fa ? ca : 0.0;
+        __syncthreads();
+        double p1 = 0.0, p2 = 0.0;                     // y1 = M 1_F, y2 = M c
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            p1 = p1 + Mr[i];
+            p2 = __builtin_fma(Mr[i], q.vc[b0 + i], p2);
+        }
+        q.part[1][h][a] = p1;
+        q.part[2][h][a] = p2;
+        __syncthreads();
+        const double y1 = q.part[1][0][a] + q.part[1][1][a];
+        const double y2 = q.part[2][0][a] + q.part[2][1][a];
+        double s1 = h == 0 && fa ? y1 : 0.0, s2 = h == 0 && fa ? y2 : 0.0, z0 = 0.0;
+        blk_sum3(q.red[0], s1, s2, z0);
+        const double lam = -((1.0 - bs) + s2) / s1;
+        const double xa = -y2 - lam * y1;
+        const bool infeas = __syncthreads_or(fa && (!(xa >= lo) || !(xa <= hi)));
+        if (!infeas) {
+            // feasible: take x; release the bound member with the most negative multiplier
+            // g_j = S[j][.] w + lam, one bound member per wave at a time
+            if (fa) wa = xa;
+            if (h == 0) q.vw[a] = wa;
+            __syncthreads();
+            double vmin = __builtin_inf();
+            int jmin = 0x7fffffff, ib = 0;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                u64 m = bnd[r];
+                while (m) {
+                    const int j = 64 * r + __builtin_ctzll(m);
+                    m &= m - 1ull;
+                    if ((ib++ & 3) != wv) continue;
+                    double g = 0.0;
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int b = lane + 64 * e;
+                        if (b < n) g = g + sh.S[tri(j, b)] * q.vw[b];
+                    }
+                    g = wave_sum(g) + lam;
+                    const double v = mbit(bhi, j) ? -g : g;
+                    if (v < vmin) { vmin = v; jmin = j; }
+                }
+            }
+            blk_argmin(q, vmin, jmin);
+            if (!(vmin < 0.0)) break;
+            // bordering by member j: s = S[.][j], u = M s, d = S_jj - s'u
+            const int j = __builtin_amdgcn_readfirstlane(jmin);
+            double up = 0.0;
+#pragma unroll
+            for (int i = 0; i < 64; ++i) {
+                const int b = b0 + i;
+                up = __builtin_fma(Mr[i], b < n ? sh.S[tri(j, b)] : 0.0, up);
+            }
+            q.part[3][h][a] = up;
+            __syncthreads();
+            const double ua = q.part[3][0][a] + q.part[3][1][a];    // 0 off the free set
+            double su = h == 0 && fa ? sh.S[tri(a, j)] * ua : 0.0, z1 = 0.0, z2 = 0.0;
+            blk_sum3(q.red[1], su, z1, z2);
+            const double rd = 1.0 / (sh.S[tri(j, j)] - su);
+            const double ut = a == j ? -1.0 : ua;
+            if (h == 0) q.vu[a] = ut;
+            __syncthreads();
+            const double utr = ut * rd;
+#pragma unroll
+            for (int i = 0; i < 64; ++i) Mr[i] = __builtin_fma(utr, q.vu[b0 + i], Mr[i]);
+            bnd[j >> 6] &= ~(1ull << (j & 63));
+            bhi[j >> 6] &= ~(1ull << (j & 63));
+            ++nf;
+        } else {
+            // ratio test: the first member (ascending index) to hit its bound along x - w
+            double amin = __builtin_inf();
+            int code = 0x7fffffff;                     // 2 * member + (bound is hi)
+            if (h == 0 && fa) {
+                const double pq = xa - wa;
+                if (xa < lo && pq < 0) {
+                    const double al = (lo - wa) / pq;
+                    if (al < 1.0) { amin = al; code = 2 * a; }
+                } else if (xa > hi && pq > 0) {
+                    const double al = (hi - wa) / pq;
+                    if (al < 1.0) { amin = al; code = 2 * a + 1; }
+                }
+            }
+            blk_argmin(q, amin, code);
+            const bool hit = code != 0x7fffffff;
+            const double alpha = hit ? amin : 1.0;
+            if (fa) wa = wa + alpha * (xa - wa);
+            if (hit) {
+                // deflation of member jb: m = M[.][jb] (= row jb)
+                const int jb = __builtin_amdgcn_readfirstlane(code >> 1);
+                const bool tohi = code & 1;
+                if (a == jb) wa = tohi ? hi : lo;
+                bnd[jb >> 6] |= 1ull << (jb & 63);
+                if (tohi) bhi[jb >> 6] |= 1ull << (jb & 63);
+                double* pub = q.pub[0];
+                if (a == jb) {
+#pragma unroll
+                    for (int i = 0; i < 64; ++i) pub[b0 + i] = Mr[i];
+                }
+                __syncthreads();
+                const double mr = pub[a] * (1.0 / pub[jb]);
+#pragma unroll
+                for (int i0 = 0; i0 < 64; i0 += 16) {
+                    double pb[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) pb[i] = pub[b0 + i0 + i];
+                    if (jb >= b0 + i0 && jb < b0 + i0 + 16) {
+#pragma unroll
+                        for (int i = 0; i < 16; ++i)
+                            Mr[i0 + i] = b0 + i0 + i == jb ? 0.0
+                                                            : __builtin_fma(-pb[i], mr, Mr[i0 + i]);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 16; ++i)
+                            Mr[i0 + i] = __builtin_fma(-pb[i], mr, Mr[i0 + i]);
+                    }
+                }
+                if (a == jb) {
+#pragma unroll
+                    for (int i = 0; i < 64; ++i) Mr[i] = 0.0;
+                }
+                --nf;
+            }
+        }
+    }
+    if (h == 0 && mem) sh.w[a] = wa;
+    if (stamps && tid == 0) stamps[7] = it;
+    __syncthreads();
+    return capped;
+}
+
 // determine_weights for one book: [rows][ld] returns (k columns, NaN = missing) -> covariance
 // (an output) and weights
 __global__ __launch_bounds__(kT) void weights_kernel(const double* R, int64_t rows, int64_t ld,
@@ -919,10 +1192,8 @@ __global__ __launch_bounds__(kT) void weights_kernel(const double* R, int64_t ro
         if (tid < k) sh.w[tid] = hi;
     } else if (k * lo >= 1.0) {
         if (tid < k) sh.w[tid] = lo;
-    } else if (!qp_setup(sh, k)) {
-        capped = true;
-    } else if (tid < 64) {
-        capped = qp_wave(sh, k, lo, hi);
+    } else {
+        capped = qp_block(sh, k, lo, hi, nullptr);
     }
     __syncthreads();
     if (tid < k) w[tid] = sh.w[tid];
@@ -1036,17 +1307,20 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
         // several passes: gather the members' window once into a contiguous [member][row]
         // scratch block, which every pass then stages with coalesced reads
         double* H = r.hscr + (i * 2 + side) * (int64_t)r.top_n * r.hrows;
-        const int64_t ne = (int64_t)k * rows;
-        for (int64_t e0 = 0; e0 < ne; e0 += 4 * kT) {
-            double v[4];
+        // (16 uncoalesced loads in flight per thread: the rows of one member are lda apart)
+        const int ne = k * (int)rows, nr = (int)rows;
+        constexpr int G = 16;
+        for (int e0 = 0; e0 < ne; e0 += G * kT) {
+            double v[G];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t e = e0 + j * kT + tid;
-                v[j] = e < ne ? gather((int)(e / rows), e % rows) : 0.0;
+            for (int j = 0; j < G; ++j) {
+                const int e = e0 + j * kT + tid;
+                const int m = (unsigned)e / (unsigned)nr;
+                v[j] = e < ne ? gather(m, e - m * nr) : 0.0;
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t e = e0 + j * kT + tid;
+            for (int j = 0; j < G; ++j) {
+                const int e = e0 + j * kT + tid;
                 if (e < ne) H[e] = v[j];
             }
         }
@@ -1073,10 +1347,15 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
     } else if (k > 0 && (r.probe & 1)) {
         if (tid < k) sh.w[tid] = 1.0 / k;
     } else if (k > 0) {
-        const bool ok = qp_setup(sh, k);
-        if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 6] = wall_clock64();
-        if (!ok) capped = true;
-        else if (tid < 64) capped = qp_wave(sh, k, r.lo, r.hi);
+        if constexpr (KM == kMaxK) {
+            capped = qp_block(sh, k, r.lo, r.hi,
+                              r.stamps ? r.stamps + (i * 2 + side) * 8 : nullptr);
+        } else {
+            const bool ok = qp_setup(sh, k);
+            if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 6] = wall_clock64();
+            if (!ok) capped = true;
+            else if (tid < 64) capped = qp_wave(sh, k, r.lo, r.hi);
+        }
     }
     if (capped && tid == 0) atomicOr(&r.status[i], 1);
     __syncthreads();
@@ -1523,6 +1802,7 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
     // books of more than one pass of member pairs re-stage their history once per pass: give
     // them a contiguous copy of their window
     const int64_t hrows = window > 0 ? window : (h_t1 > h_t0 ? h_t1 - h_t0 : 0);
+    AFM_CHECK_ARG((int64_t)top_n * hrows < (int64_t)1 << 31, "top_n x history rows over 2^31");
     double* hscr = nullptr;
     if (top_n * (top_n + 1) / 2 > kT && hrows > 0)
         AFM_HIP(hipMallocAsync((void**)&hscr, sizeof(double) * (size_t)nd * 2 * top_n * hrows,
@@ -1539,17 +1819,18 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
         AFM_HIP(hipMemcpyAsync(h.data(), r.stamps, sizeof(int64_t) * nd * 16, hipMemcpyDeviceToHost,
                                ctx->stream));
         AFM_HIP(hipStreamSynchronize(ctx->stream));
-        double acc[6] = {0, 0, 0, 0, 0, 0};
+        double acc[7] = {0, 0, 0, 0, 0, 0, 0};
         for (int64_t b = 0; b < nd * 2; ++b) {
             const int64_t* x = &h[b * 8];
             for (int j = 0; j < 4; ++j) acc[j] += (double)(x[j + 1] - x[j]);
             acc[4] += (double)(x[5] - x[1]);
             acc[5] += (double)(x[6] - x[2]);
+            acc[6] += (double)x[7];
         }
         const double f = 1.0 / (nd * 2 * 100.0);
         fprintf(stderr, "rebalance phases (us/workgroup, 100 MHz clock): select %.1f cov %.1f "
-                "(gather %.1f) qp %.1f (setup %.1f) out %.1f\n", acc[0] * f, acc[1] * f, acc[4] * f,
-                acc[2] * f, acc[5] * f, acc[3] * f);
+                "(gather %.1f) qp %.1f (setup %.1f, %.1f iterations) out %.1f\n", acc[0] * f,
+                acc[1] * f, acc[4] * f, acc[2] * f, acc[5] * f, acc[6] / (nd * 2), acc[3] * f);
         AFM_HIP(hipFree(r.stamps));
     }
     if (hscr) AFM_HIP(hipFreeAsync(hscr, ctx->stream));
