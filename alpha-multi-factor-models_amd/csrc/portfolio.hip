@@ -50,6 +50,8 @@ struct RebArgs {
     int top_n;
     double lo, hi;
     double* hscr;             // scratch [nd][2][top_n][hrows]: books' history windows (or null)
+    const double* histT;      // books over 32 names: [lda][hTn] history, member-major, NaN absent
+    int64_t hT0, hTn;         // its date range [hT0, hT0 + hTn)
     int64_t hrows;            // rows per window: window, or h_t1 - h_t0
     int probe;                // experiments (AFM_REB_PROBE): 1 skip the QP, 2 skip the covariance,
     int64_t* stamps;          // 4 phase timestamps per workgroup ([nd][2][5])
@@ -107,7 +109,7 @@ __device__ __forceinline__ int tri(int a, int b) {
 // LDS of the workgroup QP (qp_block): broadcast vectors, the two column halves' partial
 // products and the reduction slots
 struct QpLds {
-    double pub[2][128];                  // a published row of M (double-buffered in the sweep)
+    double pubk[2][4][128];              // published rows of M (block sweep: 4, double-buffered)
     double vc[128], vw[128], vu[128];    // broadcast vectors: S_FB w_B, w, u~
     double part[4][2][128];              // [product][column half][row]
     double red[6][4][4];                 // [use][wave][value]
@@ -986,37 +988,75 @@ __device__ __noinline__ bool qp_block(Shared<KM>& sh, const int n, const double 
         __syncthreads();
         return true;
     }
-    // sweep(k): A_ab -= A_ak A_kb / A_kk (a, b != k); A_ak /= A_kk; A_kk = -1 / A_kk -> A = -S^-1
-    for (int k = 0; k < n; ++k) {
-        double* pub = q.pub[k & 1];
-        if (a == k) {                                  // publish row k, then drop it
+    // Block sweep, four pivots K = [k, k + 4) per published block (sweeps compose):
+    //   A_KK <- -B^-1,  A_aK <- A_aK B^-1,  A_Kb <- B^-1 A_Kb,  A_ab <- A_ab - A_aK B^-1 A_Kb
+    // with B = A_KK (identity past n).  After all blocks A = -S^-1.  Each thread sweeps B in
+    // registers; row a then needs four coefficients: c = A_aK B^-1 off the block, and on it
+    // (a = k + p) c = e_p - B^-1[p] so the same four FMAs per element give B^-1 A_Kb.
+    const int h_u = __builtin_amdgcn_readfirstlane(h);
+    for (int k = 0; k < n; k += 4) {
+        double (*pub)[128] = q.pubk[(k >> 2) & 1];
+        if (a >= k && a < k + 4) {
 #pragma unroll
-            for (int i = 0; i < 64; ++i) pub[b0 + i] = Mr[i];
-#pragma unroll
-            for (int i = 0; i < 64; ++i) Mr[i] = 0.0;
+            for (int i = 0; i < 64; ++i) pub[a - k][b0 + i] = Mr[i];
         }
         __syncthreads();
-        // one FMA per element: row k (zeroed, pa = -1) becomes A_kb / A_kk; column k is set to
-        // pa / A_kk (-1 / A_kk on the diagonal) in the one 16-column chunk that holds it
-        const double rd = 1.0 / pub[k];
-        const double prd = (a == k ? -1.0 : pub[a]) * rd;
+        double B[4][4];
 #pragma unroll
-        for (int i0 = 0; i0 < 64; i0 += 16) {
-            double pb[16];
+        for (int x = 0; x < 4; ++x)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) pb[i] = pub[b0 + i0 + i];
-            if (k >= b0 + i0 && k < b0 + i0 + 16) {
+            for (int y = 0; y < 4; ++y)
+                B[x][y] = k + x < n && k + y < n ? pub[x][k + y] : (x == y ? 1.0 : 0.0);
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    Mr[i0 + i] = b0 + i0 + i == k ? prd : __builtin_fma(-pb[i], prd, Mr[i0 + i]);
+        for (int p = 0; p < 4; ++p) {                  // B <- -B^-1
+            const double r = 1.0 / B[p][p];
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y)
+                    if (x != p && y != p) B[x][y] = __builtin_fma(-B[x][p] * r, B[p][y], B[x][y]);
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+                if (x != p) { B[x][p] *= r; B[p][x] *= r; }
+            B[p][p] = -r;
+        }
+        const bool ink = a >= k && a < k + 4;
+        double cg[4], cv[4];                           // update coefficients, block-column values
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+            double c = 0.0;                            // A_aK B^-1 = -(A_aK (-B^-1))
+#pragma unroll
+            for (int x = 0; x < 4; ++x) c = __builtin_fma(-pub[x][a], B[x][y], c);
+            double bp = 0.0;                           // -B^-1[a - k][y]
+#pragma unroll
+            for (int x = 0; x < 4; ++x) bp = a - k == x ? B[x][y] : bp;
+            cv[y] = ink ? bp : c;
+            cg[y] = ink ? bp + (a - k == y ? 1.0 : 0.0) : c;
+        }
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            double pb[4][4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) pb[x][y] = pub[x][b0 + 4 * g + y];
+            if (64 * h_u + 4 * g == k) {
+#pragma unroll
+                for (int y = 0; y < 4; ++y) Mr[4 * g + y] = cv[y];
             } else {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) Mr[i0 + i] = __builtin_fma(-pb[i], prd, Mr[i0 + i]);
+                for (int y = 0; y < 4; ++y) {
+                    double v = Mr[4 * g + y];
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) v = __builtin_fma(-cg[x], pb[x][y], v);
+                    Mr[4 * g + y] = v;
+                }
             }
         }
     }
+    const double fin = mem ? -1.0 : 0.0;               // M = S^-1; rows past n exactly 0
 #pragma unroll
-    for (int i = 0; i < 64; ++i) Mr[i] = -Mr[i];
+    for (int i = 0; i < 64; ++i) Mr[i] *= fin;
     if (stamps && tid == 0) stamps[6] = wall_clock64();
 
     u64 bnd[2] = {0ull, 0ull}, bhi[2] = {0ull, 0ull};   // uniform: bound members, those at hi
@@ -1136,7 +1176,7 @@ __device__ __noinline__ bool qp_block(Shared<KM>& sh, const int n, const double 
                 if (a == jb) wa = tohi ? hi : lo;
                 bnd[jb >> 6] |= 1ull << (jb & 63);
                 if (tohi) bhi[jb >> 6] |= 1ull << (jb & 63);
-                double* pub = q.pub[0];
+                double* pub = q.pubk[0][0];
                 if (a == jb) {
 #pragma unroll
                     for (int i = 0; i < 64; ++i) pub[b0 + i] = Mr[i];
@@ -1296,6 +1336,17 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
             sh.S[e] = a == q ? 1e-4 : 1e-6;
         }
         __syncthreads();
+    } else if (r.histT != nullptr) {
+        if constexpr (KM == kMaxK) {
+            // each member's window is contiguous in the member-major panel: coalesced staging
+            if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 5] = wall_clock64();
+            const double* hT = r.histT + (hlo - r.hT0);
+            auto fromT = [&](int m, int64_t row) -> double {
+                return row < rows ? hT[(int64_t)bk[m] * r.hTn + row] : __builtin_nan("");
+            };
+            if (k > 32) book_cov_mfma(sh, k, rows, fromT);
+            else book_cov(sh, k, rows, fromT);
+        }
     } else if (k * (k + 1) / 2 <= kT || r.hscr == nullptr) {
         if constexpr (KM == kMaxK) {
             if (k > 32) book_cov_mfma(sh, k, rows, gather);
@@ -1772,6 +1823,35 @@ __global__ __launch_bounds__(64) void pair_union_kernel(int64_t steps, const int
 
 using namespace afm;
 
+// history rows [t0, t0 + n) of the [T][lda] panel -> member-major [lda][n], NaN where the
+// presence bit is clear (books over 32 names stage their windows from it, coalesced)
+__global__ __launch_bounds__(256) void hist_transpose_kernel(int64_t lda, int64_t A,
+                                                             const double* hist,
+                                                             const uint64_t* hbits, int64_t t0,
+                                                             int64_t n, double* hT) {
+    __shared__ double tile[64][65];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int64_t tb = (int64_t)blockIdx.x * 64, ab = (int64_t)blockIdx.y * 64;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int rr = w + 4 * j;
+        const int64_t t = t0 + tb + rr, a = ab + l;
+        double v = __builtin_nan("");
+        if (tb + rr < n && a < A) {
+            const u64 wb = hbits[(t >> 6) * lda + a];
+            const double x = hist[t * lda + a];
+            v = (wb >> (t & 63)) & 1ull ? x : v;
+        }
+        tile[rr][l] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int c = w + 4 * j;
+        if (tb + l < n) hT[(ab + c) * n + tb + l] = tile[l][c];
+    }
+}
+
 template <int KM>
 static int launch_rebalance(afm_ctx* ctx, const RebArgs& r) {
     const size_t smem = sizeof(Shared<KM>);
@@ -1804,11 +1884,27 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
     const int64_t hrows = window > 0 ? window : (h_t1 > h_t0 ? h_t1 - h_t0 : 0);
     AFM_CHECK_ARG((int64_t)top_n * hrows < (int64_t)1 << 31, "top_n x history rows over 2^31");
     double* hscr = nullptr;
-    if (top_n * (top_n + 1) / 2 > kT && hrows > 0)
+    double* histT = nullptr;
+    int64_t hT0 = 0, hTn = 0;
+    if (top_n > 32) {
+        // books over 32 names: the history panel member-major once, instead of a strided gather
+        // per book (each member's window then one contiguous run)
+        hT0 = window > 0 ? 0 : h_t0;
+        hTn = window > 0 ? T : (h_t1 > h_t0 ? h_t1 - h_t0 : 0);
+        if (hTn > 0) {
+            AFM_HIP(hipMallocAsync((void**)&histT, sizeof(double) * (size_t)lda * hTn,
+                                   ctx->stream));
+            hipLaunchKernelGGL(hist_transpose_kernel, dim3((unsigned)((hTn + 63) / 64),
+                                                           (unsigned)(lda / 64)),
+                               dim3(256), 0, ctx->stream, lda, A, hist, hist_bits, hT0, hTn, histT);
+            AFM_HIP(hipGetLastError());
+        }
+    } else if (top_n * (top_n + 1) / 2 > kT && hrows > 0)
         AFM_HIP(hipMallocAsync((void**)&hscr, sizeof(double) * (size_t)nd * 2 * top_n * hrows,
                                ctx->stream));
     RebArgs r{T, lda, A, dates, nd, pred, trad_bits, hist, hist_bits, h_t0, h_t1, window, close,
-              tmr, top_n, lo, hi, hscr, hrows, 0, nullptr, k_out, books, weights, sums, upos, usize, status};
+              tmr, top_n, lo, hi, hscr, histT, hT0, hTn, hrows, 0, nullptr, k_out, books, weights,
+              sums, upos, usize, status};
 #ifdef AFM_PROBE                     // profiling build (make prof): phase experiments
     if (const char* e = getenv("AFM_REB_PROBE")) r.probe = atoi(e);
 #endif
@@ -1834,6 +1930,7 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
         AFM_HIP(hipFree(r.stamps));
     }
     if (hscr) AFM_HIP(hipFreeAsync(hscr, ctx->stream));
+    if (histT) AFM_HIP(hipFreeAsync(histT, ctx->stream));
     return rc;
 }
 
