@@ -23,6 +23,7 @@
 //   -> 0 included, evaluated sparsely at the members' union positions).
 #include "afm_internal.h"
 
+#include <type_traits>
 #include <vector>
 
 #pragma clang fp contract(off)
@@ -129,15 +130,18 @@ struct Shared {
     double w[KM], x[KM], c[KM];
     double sinv[258];                    // 1 / n for the Welford updates (n <= 257)
     double S[KM * (KM + 1) / 2];
-    u64 pm[KM];                          // presence words of the staged chunk (MFMA covariance)
+    u64 pm[KM > 32 ? KM : 1];            // presence words of the staged chunk (MFMA covariance)
     union {
         double hv[KM][65];               // staged history chunk [member][date]
         double L[KM * (KM + 1) / 2];     // Cholesky factor of S_FF (packed by member pair)
-        QpLds qp;                        // the workgroup QP of books of more than 32 names
+        // the workgroup QP of books of more than 32 names (absent from the 32-name layout, whose
+        // LDS size sets how many headline workgroups share a CU)
+        typename std::conditional<(KM > 32), QpLds, char>::type qp;
     } u;
 };
 
 static_assert(sizeof(Shared<kMaxK>) <= 160 * 1024, "rebalance LDS over the CU's 160 KB");
+static_assert(sizeof(Shared<32>) <= 40 * 1024, "headline rebalance LDS: 4 workgroups per CU");
 
 // Welford pairwise-complete covariance (pandas nancorr(cov=True), KKT:821-822: rows in date
 // order, a pair's rows where both values are finite) of the k members' history rows [0, rows)
