@@ -247,29 +247,6 @@ struct CovPairs {
     }
 };
 
-// stage rows [h0, h0 + 64) of the k members into sh.u.hv (NaN past the window), with each
-// member's presence word (bit d: row h0 + d finite) in sh.pm
-template <int KM, class Get>
-__device__ __forceinline__ void cov_stage(Shared<KM>& sh, const int k, const int64_t h0, Get get) {
-    constexpr int EPT = KM * 64 / kT;
-    const int tid = threadIdx.x;
-    double v[EPT];
-#pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-        const int e = tid + j * kT;
-        v[j] = e < k * 64 ? get(e >> 6, h0 + (e & 63)) : 0.0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-        const int e = tid + j * kT;                  // member e >> 6 (uniform per wave), row lane
-        const u64 m = __ballot(e < k * 64 && __builtin_isfinite(v[j]));
-        if (e < k * 64) sh.u.hv[e >> 6][e & 63] = v[j];
-        if ((tid & 63) == 0 && e < k * 64) sh.pm[e >> 6] = m;
-    }
-    __syncthreads();
-}
-
 template <int KM, int W, class Get>
 __device__ __noinline__ void cov_mfma_wave(Shared<KM>& sh, const int k, const int64_t rows,
                                            Get get) {
@@ -290,8 +267,30 @@ __device__ __noinline__ void cov_mfma_wave(Shared<KM>& sh, const int k, const in
 #pragma unroll
         for (int r = 0; r < 4; ++r) nn[s][r] = 0;
     }
+    // software-pipelined staging: chunk c + 1 is loaded into registers while chunk c is multiplied
+    constexpr int EPT = KM * 64 / kT;
+    double v[EPT];
+    auto load = [&](int64_t h0) {                  // branch-free: every load in flight at once
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int e = tid + j * kT;
+            const int m = (e >> 6) < k ? (e >> 6) : k - 1;
+            const double x = get(m, h0 + (e & 63));
+            v[j] = e < k * 64 ? x : 0.0;
+        }
+    };
+    if (rows > 0) load(0);
     for (int64_t h0 = 0; h0 < rows; h0 += 64) {
-        cov_stage(sh, k, h0, get);
+        __syncthreads();                             // the previous chunk's readers are done
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int e = tid + j * kT;              // member e >> 6 (uniform per wave), row lane
+            const u64 mk = __ballot(e < k * 64 && __builtin_isfinite(v[j]));
+            if (e < k * 64) sh.u.hv[e >> 6][e & 63] = v[j];
+            if (lane == 0 && e < k * 64) sh.pm[e >> 6] = mk;
+        }
+        __syncthreads();
+        if (h0 + 64 < rows) load(h0 + 64);
         if (h0 == 0) {                               // centring constants
             if (tid < k) {
                 double c0 = 0.0;
@@ -976,7 +975,10 @@ __device__ __noinline__ bool qp_block(Shared<KM>& sh, const int n, const double 
                                      const double hi, int64_t* stamps) {
     static_assert(KM == 128 && kT == 256, "qp_block: 128 member rows x 2 column halves");
     QpLds& q = sh.u.qp;
-    const int tid = threadIdx.x, a = tid & 127, h = tid >> 7, b0 = 64 * h;
+    // the column half is uniform per wave: column indices, their LDS addresses and the S row
+    // reads of the bordering step are scalar
+    const int tid = threadIdx.x, a = tid & 127;
+    const int h = __builtin_amdgcn_readfirstlane(tid >> 7), b0 = 64 * h;
     const int wv = tid >> 6, lane = tid & 63;
     const bool mem = a < n;
     double Mr[64];
@@ -997,7 +999,6 @@ __device__ __noinline__ bool qp_block(Shared<KM>& sh, const int n, const double 
     // with B = A_KK (identity past n).  After all blocks A = -S^-1.  Each thread sweeps B in
     // registers; row a then needs four coefficients: c = A_aK B^-1 off the block, and on it
     // (a = k + p) c = e_p - B^-1[p] so the same four FMAs per element give B^-1 A_Kb.
-    const int h_u = __builtin_amdgcn_readfirstlane(h);
     for (int k = 0; k < n; k += 4) {
         double (*pub)[128] = q.pubk[(k >> 2) & 1];
         if (a >= k && a < k + 4) {
@@ -1044,7 +1045,7 @@ __device__ __noinline__ bool qp_block(Shared<KM>& sh, const int n, const double 
             for (int x = 0; x < 4; ++x)
 #pragma unroll
                 for (int y = 0; y < 4; ++y) pb[x][y] = pub[x][b0 + 4 * g + y];
-            if (64 * h_u + 4 * g == k) {
+            if (b0 + 4 * g == k) {
 #pragma unroll
                 for (int y = 0; y < 4; ++y) Mr[4 * g + y] = cv[y];
             } else {
@@ -1344,9 +1345,13 @@ __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
         if constexpr (KM == kMaxK) {
             // each member's window is contiguous in the member-major panel: coalesced staging
             if (r.stamps && tid == 0) r.stamps[(i * 2 + side) * 8 + 5] = wall_clock64();
+            // captured by value: the covariance is a called function, and references into the
+            // kernel arguments would be reloaded at every element
             const double* hT = r.histT + (hlo - r.hT0);
-            auto fromT = [&](int m, int64_t row) -> double {
-                return row < rows ? hT[(int64_t)bk[m] * r.hTn + row] : __builtin_nan("");
+            const int64_t ld = r.hTn;
+            auto fromT = [hT, ld, bk, rows](int m, int64_t row) -> double {
+                const double x = hT[(int64_t)bk[m] * ld + (row < rows ? row : 0)];
+                return row < rows ? x : __builtin_nan("");
             };
             if (k > 32) book_cov_mfma(sh, k, rows, fromT);
             else book_cov(sh, k, rows, fromT);
