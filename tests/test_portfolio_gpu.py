@@ -186,10 +186,12 @@ def test_bootstrap_paths_vs_oracle(top_n, window, npaths):
     assert same(got["turnover"][2, 1:], np.asarray(pm.turnovers[1:], dtype=np.float64))
 
 
-@pytest.mark.parametrize("k,holes", [(64, False), (100, False), (100, True), (128, False)])
+@pytest.mark.parametrize("k,holes", [(33, False), (37, True), (50, False), (64, False),
+                                     (100, False), (100, True), (127, True), (128, False)])
 def test_large_book_weights_vs_oracle(k, holes):
     """determine_weights for the survey's stress book sizes (top_n = 100): the
-    active-set QP with its incrementally updated Cholesky factor against the oracle's
+    workgroup active-set QP (S_FF^-1 in registers, four-pivot block sweep -- sizes that are not
+    a multiple of 4 pad the last block) and the one-pass MFMA covariance against the oracle's
     refactor-every-step solve, rel 1e-9; identical bound sets."""
     from afm.portfolio import min_variance_weights
     from oracle import portfolio as P
