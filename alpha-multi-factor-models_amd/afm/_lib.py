@@ -24,6 +24,9 @@ SIGNATURES = {
     "afm_ctx_create": (I32, [I32, ctypes.POINTER(P)]),
     "afm_ctx_set_stream": (I32, [P, P]),
     "afm_ctx_set_option": (I32, [P, ctypes.c_char_p, I64]),
+    "afm_ctx_get_option": (I32, [P, ctypes.c_char_p, ctypes.POINTER(I64)]),
+    "afm_stream_create_cu_mask": (I32, [I32, P, I32, ctypes.POINTER(P)]),
+    "afm_stream_destroy": (I32, [P]),
     "afm_ctx_destroy": (I32, [P]),
     "afm_last_error": (ctypes.c_char_p, []),
     "afm_version": (I32, []),
@@ -135,6 +138,13 @@ class Context:
         check(lib().afm_ctx_set_option(self.handle, name.encode(), int(value)),
               f"afm_ctx_set_option({name})")
 
+    def get_option(self, name: str) -> int:
+        """afm_ctx_get_option: the current value of an execution option."""
+        v = I64()
+        check(lib().afm_ctx_get_option(self.handle, name.encode(), ctypes.byref(v)),
+              f"afm_ctx_get_option({name})")
+        return int(v.value)
+
     def bind_stream(self):
         import torch
         s = torch.cuda.current_stream(self.device).cuda_stream
@@ -156,7 +166,8 @@ def factor_names() -> list:
 
 class options:
     """Context manager: execution options of the device's context (afm_ctx_set_option) for the
-    duration of a block, restored to the defaults after -- the invariance tests' work splits."""
+    duration of a block, restored after it to the values they had before (nesting-safe) -- the
+    invariance tests' work splits."""
 
     DEFAULTS = {"factor_split": 0, "factor_pair": 1, "factor_fast": 1, "gram_checked": 0}
 
@@ -165,11 +176,46 @@ class options:
 
     def __enter__(self):
         self.ctx = Context.get(self.device)
+        self.saved = {k: self.ctx.get_option(k) for k in self.opts}
         for k, v in self.opts.items():
             self.ctx.set_option(k, v)
         return self.ctx
 
     def __exit__(self, *exc):
-        for k in self.opts:
-            self.ctx.set_option(k, self.DEFAULTS[k])
+        for k, v in self.saved.items():
+            self.ctx.set_option(k, v)
         return False
+
+
+def cu_mask_stream(device: int, exclude: int):
+    """A torch stream on ``device`` whose kernels avoid ``exclude`` compute units (spread evenly
+    over the logical CU mask), made by afm_stream_create_cu_mask; the pipeline's FM side stream
+    (PipelineConfig.fm_free_cus).  The stream lives as long as the returned object."""
+    import torch
+    n = torch.cuda.get_device_properties(device).multi_processor_count
+    if not 0 < exclude < n:
+        raise AfmError(f"exclude must be in 1..{n - 1} compute units")
+    keep = [True] * n
+    for i in range(exclude):                       # every (n / exclude)-th CU left free
+        keep[(i * n) // exclude] = False
+    words = (ctypes.c_uint32 * ((n + 31) // 32))()
+    for i, k in enumerate(keep):
+        if k:
+            words[i // 32] |= 1 << (i % 32)
+    h = P()
+    check(lib().afm_stream_create_cu_mask(device, words, len(words), ctypes.byref(h)),
+          "afm_stream_create_cu_mask")
+    return _MaskedStream(device, h)
+
+
+class _MaskedStream:
+    def __init__(self, device, handle):
+        import torch
+        self.handle = handle
+        self.stream = torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", device))
+
+    def __del__(self):
+        try:
+            lib().afm_stream_destroy(self.handle)
+        except Exception:
+            pass

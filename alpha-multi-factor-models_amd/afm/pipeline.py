@@ -107,6 +107,10 @@ class PipelineConfig:
     labels_side: bool = True
     fm_fork: str = "predict"
     main_priority: bool = True
+    # fm_free_cus -- the FM side stream's kernels avoid this many compute units (a CU-masked
+    # stream, afm_stream_create_cu_mask), so the latency-bound tail beside the FM MFMA Grams keeps
+    # whole CUs; 0 = an ordinary stream
+    fm_free_cus: int = 0
 
 
 @dataclass
@@ -351,7 +355,11 @@ class Pipeline:
             raise ValueError(f"fm_fork={c.fm_fork!r}: expected gram, predict, analyzer or "
                              "rebalance")
         self.main = torch.cuda.Stream(device=dev, priority=-8 if c.main_priority else 0)
-        self.side = torch.cuda.Stream(device=dev, priority=0)
+        if c.fm_free_cus > 0:
+            self._side_owner = _lib.cu_mask_stream(dev.index, c.fm_free_cus)
+            self.side = self._side_owner.stream
+        else:
+            self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
         self.labels_done = torch.cuda.Event()
 

@@ -65,6 +65,36 @@ int afm_ctx_set_option(afm_ctx* ctx, const char* name, int64_t value) {
     return AFM_OK;
 }
 
+int afm_ctx_get_option(afm_ctx* ctx, const char* name, int64_t* value) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(name != nullptr && value != nullptr, "null argument");
+    const std::string n(name);
+    if (n == "factor_split") *value = ctx->factor_split;
+    else if (n == "factor_pair") *value = ctx->factor_pair ? 1 : 0;
+    else if (n == "factor_fast") *value = ctx->factor_fast ? 1 : 0;
+    else if (n == "gram_checked") *value = ctx->gram_checked ? 1 : 0;
+    else AFM_CHECK_ARG(false, "unknown option " + n);
+    return AFM_OK;
+}
+
+int afm_stream_create_cu_mask(int device, const uint32_t* cu_mask, int nwords, void** out) {
+    AFM_CHECK_ARG(out != nullptr && cu_mask != nullptr && nwords > 0, "null argument");
+    int n = 0;
+    AFM_HIP(hipGetDeviceCount(&n));
+    AFM_CHECK_ARG(device >= 0 && device < n, "device ordinal out of range");
+    AFM_HIP(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    AFM_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, cu_mask));
+    *out = (void*)s;
+    return AFM_OK;
+}
+
+int afm_stream_destroy(void* stream) {
+    AFM_CHECK_ARG(stream != nullptr, "null stream");
+    AFM_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+    return AFM_OK;
+}
+
 int afm_ctx_destroy(afm_ctx* ctx) {
     if (!ctx || ctx->magic != 0x61666d31) {
         afm_set_error("afm_ctx_destroy: invalid afm_ctx");

@@ -153,19 +153,28 @@ __device__ double leaf_sum(const double* a, int n) {
     return res;
 }
 
-// np.add.reduce of v[0..n) (0.0 + numpy pairwise sum), evaluated by the whole block
+// np.add.reduce of v[0..n) -- the identity 0.0, then numpy's pairwise sums of the consecutive
+// kNpBuf-element buffers of the ufunc's buffered reduction added one by one (over 8192 elements
+// the sum is not one pairwise tree: oracle np_sum, pinned to numpy in tests/test_oracle_golden.py)
+// -- evaluated by the whole block
+constexpr int64_t kNpBuf = 8192;
 template <int NT = kT>
 __device__ double block_np_sum(PwShared& p, const double* v, int64_t n) {
     const int tid = threadIdx.x;
     if (tid == 0) {
         p.nleaves = 0;
         p.cursor = 0;
-        if (n > 0) pw_enum(p, 0, n);
+        for (int64_t c0 = 0; c0 < n; c0 += kNpBuf) pw_enum(p, c0, n - c0 < kNpBuf ? n - c0 : kNpBuf);
     }
     __syncthreads();
     for (int l = tid; l < p.nleaves; l += NT) p.lval[l] = leaf_sum(v + p.loff[l], p.llen[l]);
     __syncthreads();
-    if (tid == 0) p.result = n > 0 ? 0.0 + pw_combine(p, n) : 0.0;
+    if (tid == 0) {
+        double r = 0.0;
+        for (int64_t c0 = 0; c0 < n; c0 += kNpBuf)
+            r = r + pw_combine(p, n - c0 < kNpBuf ? n - c0 : kNpBuf);
+        p.result = r;
+    }
     __syncthreads();
     double r = p.result;
     __syncthreads();
@@ -204,11 +213,11 @@ struct PrepShared {
 // One workgroup (4 waves) per date.  The three row masks of KKT:313's merge + dropna steps as
 // bit words by ballot over coalesced 64-asset segments, and their prefix counts.  Then per
 // return column: its rows compacted (ascending security id) into the scratch row, numpy's
-// pairwise summation tree of that length built level by level (node m > 128 splits at
-// m/2 - (m/2)%8, as in numpy's pairwise_sum), every leaf summed by its own thread (the
+// pairwise summation tree of each 8192-row reduction buffer built level by level (node m > 128
+// splits at m/2 - (m/2)%8, as in numpy's pairwise_sum), every leaf summed by its own thread (the
 // 8-accumulator block, or the plain loop under 8), the internal nodes added bottom-up level by
-// level: mean = (0.0 + sum) / n bit-exactly, with no serial walk of the tree.  Finally the rows
-// surviving all three steps are written compacted with demeaned returns.
+// level, the buffers added one by one onto 0.0: mean = sum / n bit-exactly, with no serial
+// walk.  Finally the rows surviving all three steps are written compacted with demeaned returns.
 __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
     __shared__ PrepShared sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -271,11 +280,14 @@ __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
             if ((m >> lane) & 1ull)
                 scr[sh.pre[q][w] + __popcll(m & ((1ull << lane) - 1ull))] = x[(int64_t)w * 64 + lane];
         }
+        const int nbuf = n > 0 ? (int)((n + kNpBuf - 1) / kNpBuf) : 1;   // level 0: the buffers
+        if (tid < nbuf) {
+            sh.noff[tid] = (int)(tid * kNpBuf);
+            sh.nlen[tid] = n - tid * kNpBuf < kNpBuf ? (int)(n - tid * kNpBuf) : (int)kNpBuf;
+        }
         if (tid == 0) {
-            sh.noff[0] = 0;
-            sh.nlen[0] = n;
             sh.lvl[0] = 0;
-            sh.lvl[1] = 1;
+            sh.lvl[1] = nbuf;
         }
         __syncthreads();
         int nlev = 0;
@@ -337,7 +349,11 @@ __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
             }
             __syncthreads();
         }
-        if (tid == 0) sh.mu[q] = n > 0 ? (0.0 + sh.nval[0]) / (double)n : qnan();
+        if (tid == 0) {                                  // the buffers added one by one
+            double r = 0.0;
+            for (int c = 0; c < nbuf; ++c) r = r + sh.nval[c];
+            sh.mu[q] = n > 0 ? r / (double)n : qnan();
+        }
         __syncthreads();
     }
     if (g.stamps && tid == 0) g.stamps[t * 5 + 3] = wall_clock64();
@@ -866,11 +882,16 @@ __global__ __launch_bounds__(128) void xs_stats_kernel(StatArgs g) {
 }
 
 // ---- series: cumulative layers / long-short / top-k, per-year IR -----------------------------
-__device__ double seq_pairwise(const double* a, int64_t n) {   // np.add.reduce, single thread
+__device__ double seq_pairwise(const double* a, int64_t n) {   // numpy pairwise_sum, one thread
     if (n <= 128) return leaf_sum(a, (int)n);
     int64_t n2 = n / 2;
     n2 -= n2 % 8;
     return seq_pairwise(a, n2) + seq_pairwise(a + n2, n - n2);
+}
+__device__ double seq_np_sum(const double* a, int64_t n) {      // np.add.reduce (block_np_sum)
+    double r = 0.0;
+    for (int64_t c0 = 0; c0 < n; c0 += kNpBuf) r = r + seq_pairwise(a + c0, n - c0 < kNpBuf ? n - c0 : kNpBuf);
+    return r;
 }
 
 // One workgroup.  Every series is a sequential recurrence over the dates, so each runs in one
@@ -961,15 +982,15 @@ __global__ __launch_bounds__(1024) void xs_series_kernel(int64_t nd, const doubl
         }
         double res = qnan();
         if (n > 0) {
-            const double mean = (0.0 + seq_pairwise(buf, n)) / (double)n;
+            const double mean = seq_np_sum(buf, n) / (double)n;
             double sd = qnan();
             if (n > 1) {
-                const double avg = (0.0 + seq_pairwise(buf, n)) / (double)n;
+                const double avg = seq_np_sum(buf, n) / (double)n;
                 for (int64_t i = 0; i < n; ++i) {
                     const double d = avg - buf[i];
                     buf[i] = d * d;
                 }
-                sd = __builtin_sqrt((0.0 + seq_pairwise(buf, n)) / ((double)n - 1.0));
+                sd = __builtin_sqrt(seq_np_sum(buf, n) / ((double)n - 1.0));
             }
             res = mean / sd;
         }

@@ -169,6 +169,35 @@ struct Runs {
     Run C, V, VP, VC, R, X, Y, XY;
 };
 
+// ---- output stores --------------------------------------------------------------------------
+// Lanes and assets (round 4): lane i < 32 holds asset 2i of its 64-asset block, lane i + 32 asset
+// 2i + 1 (lane_asset).  A step's output values are stored two columns at a time: after
+// v_permlane32_swap of the two values, lane i holds BOTH assets of the first column and lane
+// i + 32 both assets of the second, so one 16-B store per lane writes 512 contiguous bytes of
+// each column's row -- half the store instructions of one 8-B store per column (at config C the
+// kernel is bound by its write stream meeting the recurrences).  The stores run
+// with the whole wave active after the day's (divergent) step: a lane absent that day writes NaN
+// into its cells.
+__device__ __forceinline__ int lane_asset(int lane) { return 2 * (lane & 31) + (lane >> 5); }
+
+// the columns a job writes, as a 96-bit mask (lo: columns 0-63, hi: 64-95)
+struct Cols {
+    u64 lo, hi;
+};
+constexpr Cols col1(int c) { return c < 64 ? Cols{1ull << c, 0} : Cols{0, 1ull << (c - 64)}; }
+constexpr Cols operator|(Cols a, Cols b) { return Cols{a.lo | b.lo, a.hi | b.hi}; }
+constexpr int ncols(Cols m) { return __builtin_popcountll(m.lo) + __builtin_popcountll(m.hi); }
+struct ColList {
+    int c[96];
+};
+constexpr ColList col_list(Cols m) {
+    ColList l{};
+    int n = 0;
+    for (int c = 0; c < 96; ++c)
+        if (c < 64 ? ((m.lo >> c) & 1ull) : ((m.hi >> (c - 64)) & 1ull)) l.c[n++] = c;
+    return l;
+}
+
 // Per-lane view of one (asset, present day) step.  Lookback L reads observation p - L.
 struct Step {
     const LDS Smem* sm;
@@ -176,9 +205,12 @@ struct Step {
     Runs* rn;
     int64_t plane;
     uint32_t voff, pmoff;      // asset * 8; (pm * kLanes + lane) * 8 (pm = p mod kRing)
+    uint32_t poff;             // (block * 64 + 2 * (lane & 31)) * 8: the lane's asset pair
+    int64_t hmask;             // lane >= 32 ? -1 : 0
     int lane, p;
     bool anynan, anybad;
     double r0, g0;             // ret(p), vol_change(p), computed once per step when needed
+    double ov[96];             // the step's output values by column (only the pack's are used)
     __device__ __forceinline__ double C(int L) const {
         return *(const LDS double*)((const LDS char*)&sm->c[0][0] + ring_off(pmoff, L));
     }
@@ -186,24 +218,54 @@ struct Step {
         return *(const LDS double*)((const LDS char*)&sm->v[0][0] + ring_off(pmoff, L));
     }
     __device__ __forceinline__ double div(double x, int n) const { return div_n(sm, x, n); }
-    // buffer_store with an SGPR descriptor based at this day's column row and the lane's 32-bit
-    // byte offset: no per-store address arithmetic on the VALU, and (unlike an inline-asm store)
-    // the scheduler may place the store anywhere after its value (11.8-12.2 -> 11.2-11.4 ms at
-    // config C, bit-identical).  Raw buffer, stride 0: num_records bounds the byte offset
-    // (< lda * 8); word 3 = 0x00020000, the CDNA raw-buffer format word.
-    __device__ __forceinline__ void store(int col, double x) {
+    __device__ __forceinline__ void put(int col, double x) {
+        ov[col] = x;
+        anynan |= (x != x);
+        anybad |= !__builtin_isfinite(x);
+    }
+    // fast step: columns that are finite on a clean day need no NaN / inf bookkeeping
+    __device__ __forceinline__ void putf(int col, double x) { ov[col] = x; }
+    // before the day's step: the pack's columns NaN (what an absent lane stores)
+    template <u64 LO, u64 HI>
+    __device__ __forceinline__ void reset() {
+        constexpr Cols m{LO, HI};
+        constexpr int n = ncols(m);
+        constexpr ColList l = col_list(m);
+#pragma unroll
+        for (int k = 0; k < n; ++k) ov[l.c[k]] = qnan();
+    }
+    // one column, 8 B per lane: a buffer_store with an SGPR descriptor based at the column row and
+    // the lane's 32-bit byte offset (the scheduler may place it anywhere after its value; raw
+    // buffer, num_records bounds the offset; word 3 = 0x00020000, the CDNA raw-buffer format)
+    __device__ __forceinline__ void store1(int col, double x) {
         typedef unsigned v2u __attribute__((ext_vector_type(2)));
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(out + col * plane), 0, 0x7fffffff, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, x), r, (int)voff, 0, 0);
     }
-    __device__ __forceinline__ void put(int col, double x) {
-        store(col, x);
-        anynan |= (x != x);
-        anybad |= !__builtin_isfinite(x);
+    // two columns, 16 B per lane (see lane_asset)
+    __device__ __forceinline__ void store2(int c1, double x1, int c2, double x2) {
+        typedef unsigned v2u __attribute__((ext_vector_type(2)));
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v2u a = __builtin_bit_cast(v2u, x1), b = __builtin_bit_cast(v2u, x2);
+        const auto l = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+        const v4u w = {l[0], h[0], l[1], h[1]};
+        // the upper half-wave's row: the first column's row + (c2 - c1) planes (uniform), masked
+        const int64_t d = (int64_t)(c2 - c1) * plane * 8;
+        GLB char* row = (GLB char*)(out + c1 * plane) + (d & hmask);
+        *(GLB v4u*)(row + poff) = w;
     }
-    // fast step: columns that are finite on a clean day need no NaN / inf bookkeeping
-    __device__ __forceinline__ void putf(int col, double x) { store(col, x); }
+    // after the day's step, the whole wave active: the pack's columns in pairs
+    template <u64 LO, u64 HI>
+    __device__ __forceinline__ void flush() {
+        constexpr Cols m{LO, HI};
+        constexpr int n = ncols(m);
+        constexpr ColList l = col_list(m);
+#pragma unroll
+        for (int k = 0; k + 1 < n; k += 2) store2(l.c[k], ov[l.c[k]], l.c[k + 1], ov[l.c[k + 1]]);
+        if constexpr ((n & 1) != 0) store1(l.c[n - 1], ov[l.c[n - 1]]);
+    }
     // close.pct_change() at lookback L, with the window kernels' inf -> NaN (_prep_values)
     __device__ __forceinline__ double ret(int L) const {
         if (L == 0) return r0;
@@ -469,6 +531,7 @@ struct ComC {
 template <int W>
 struct Sma {  // No-talib.py:9-10
     static constexpr u64 kC = lb(0) | lb(W), kV = 0;
+    static constexpr Cols kOut = col1((W - 6) / 4);
     RollMean m;
     __device__ void init() { m.init(); }
     __device__ void step(Step& s) {
@@ -491,6 +554,7 @@ struct Sma {  // No-talib.py:9-10
 template <int W>
 struct Ema {  // No-talib.py:13-14
     static constexpr u64 kC = lb(0), kV = 0;
+    static constexpr Cols kOut = col1(12 + (W - 6) / 4);
     Ewm e;
     __device__ void init() { e.init(); }
     __device__ void step(Step& s) {
@@ -507,6 +571,7 @@ struct Ema {  // No-talib.py:13-14
 template <int W>
 struct Vwma {  // No-talib.py:17-19
     static constexpr u64 kC = lb(0) | lb(W), kV = lb(0) | lb(W);
+    static constexpr Cols kOut = col1(24 + (W - 6) / 4);
     RollMean mvc, mv;
     __device__ void init() { mvc.init(); mv.init(); }
     __device__ void step(Step& s) {
@@ -544,6 +609,7 @@ struct Vwma {  // No-talib.py:17-19
 template <int W>
 struct Bbands {  // No-talib.py:22-26
     static constexpr u64 kC = lb(0) | lb(W), kV = 0;
+    static constexpr Cols kOut = col1(36 + 2 * ((W - 14) / 6)) | col1(37 + 2 * ((W - 14) / 6));
     RollMean m;
     RollVar v;
     __device__ void init() { m.init(); v.init(); }
@@ -589,6 +655,8 @@ struct Bbands {  // No-talib.py:22-26
 template <int W>
 struct MomAccelRocr {  // No-talib.py:35-44
     static constexpr u64 kC = lb(0) | lb(1) | lb(W) | lb(W + 1), kV = 0;
+    static constexpr Cols kOut = col1(52 + (W - 14) / 6) | col1(60 + (W - 14) / 6) |
+                                 col1(68 + (W - 14) / 6);
     __device__ void init() {}
     __device__ void step(Step& s) {
         const int k = (W - 14) / 6;
@@ -624,6 +692,7 @@ struct MomAccelRocr {  // No-talib.py:35-44
 template <int SLOW>
 struct Macd {  // No-talib.py:47-50
     static constexpr u64 kC = lb(0), kV = 0;
+    static constexpr Cols kOut = col1(76 + (SLOW - 18) / 6);
     Ewm fast, slow;
     __device__ void init() { fast.init(); slow.init(); }
     __device__ void step(Step& s) {
@@ -649,6 +718,7 @@ struct Macd {  // No-talib.py:47-50
 template <int I>
 struct Rsi {  // No-talib.py:53-59
     static constexpr u64 kC = lb(0) | lb(1), kV = 0;
+    static constexpr Cols kOut = col1(79 + (I - 8) / 6);
     Ewm up, dn;
     __device__ void init() { up.init(); dn.init(); }
     __device__ void step(Step& s) {
@@ -684,6 +754,7 @@ struct Rsi {  // No-talib.py:53-59
 
 struct PvtObvPsy {  // No-talib.py:62-69
     static constexpr u64 kC = lb(0) | lb(1) | lb(14) | lb(15), kV = lb(0);
+    static constexpr Cols kOut = col1(82) | col1(83) | col1(84);
     double pvt, obv;
     int ups;
     __device__ void init() { pvt = 0.0; obv = 0.0; ups = 0; }
@@ -758,6 +829,7 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
 struct RetSd3 {
     RetSd<3, 85> a;
     static constexpr u64 kC = RetSd<3, 85>::kC, kV = 0;
+    static constexpr Cols kOut = col1(85);
     __device__ void init() { a.init(); }
     __device__ void step(Step& s) { a.step(s); }
     template <class S> __device__ void fstep(S& s) { a.fstep(s); }
@@ -768,6 +840,7 @@ struct RetSd5x15 {  // sd_5, sd_15, sd5_15
     RetSd<5, 86> a;
     RetSd<15, 87> b;
     static constexpr u64 kC = RetSd<5, 86>::kC | RetSd<15, 87>::kC, kV = 0;
+    static constexpr Cols kOut = col1(86) | col1(87) | col1(88);
     __device__ void init() { a.init(); b.init(); }
     __device__ void step(Step& s) {
         double x = a.step(s), y = b.step(s);
@@ -814,6 +887,7 @@ struct VolSd {  // volsd_W (No-talib.py:79-80)
 struct VolSd3 {
     VolSd<3, 89> a;
     static constexpr u64 kC = 0, kV = VolSd<3, 89>::kV;
+    static constexpr Cols kOut = col1(89);
     __device__ void init() { a.init(); }
     __device__ void step(Step& s) { a.step(s); }
     template <class S> __device__ void fstep(S& s) { a.fstep(s); }
@@ -824,6 +898,7 @@ struct VolSd5x15 {
     VolSd<5, 90> a;
     VolSd<15, 91> b;
     static constexpr u64 kC = 0, kV = VolSd<5, 90>::kV | VolSd<15, 91>::kV;
+    static constexpr Cols kOut = col1(90) | col1(91) | col1(92);
     __device__ void init() { a.init(); b.init(); }
     __device__ void step(Step& s) {
         double x = a.step(s), y = b.step(s);
@@ -844,6 +919,7 @@ struct VolSd5x15 {
 template <int W, bool WITH_VC>
 struct Corr {
     static constexpr u64 kC = lb(W) | lb(W + 1), kV = lb(W) | lb(W + 1);
+    static constexpr Cols kOut = col1(94 + (W == 15 ? 1 : 0)) | (WITH_VC ? col1(93) : Cols{0, 0});
     RollMean mxy, mx, my;
     RollVar vx, vy;
     int cnt;
@@ -958,6 +1034,7 @@ template <>
 struct Pack<> {
     static constexpr unsigned kSer = 0;
     static constexpr u64 kC = 0, kV = 0;
+    static constexpr Cols kOut{0, 0};
     __device__ void init() {}
     __device__ void step(Step&) {}
     template <class S> __device__ void fstep(S&) {}
@@ -968,6 +1045,7 @@ struct Pack<H, R...> {
     static constexpr unsigned kSer = Ser<H>::value | Pack<R...>::kSer;
     // the lookbacks the jobs' clean / warm steps read
     static constexpr u64 kC = H::kC | Pack<R...>::kC, kV = H::kV | Pack<R...>::kV;
+    static constexpr Cols kOut = H::kOut | Pack<R...>::kOut;
     H h;
     Pack<R...> r;
     __device__ void init() { h.init(); r.init(); }
@@ -1021,7 +1099,7 @@ using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>, Ema<6>>;
 __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane, int64_t block,
                                           GLB double* st) {
     LDS Smem& sm = *smp;
-    const int64_t asset = block * kLanes + lane;
+    const int64_t asset = block * kLanes + lane_asset(lane);
     const int c0 = a.c0, nch = a.c1;
     double pc[kChunk], pv[kChunk];
     u64 vb = a.vbits[(int64_t)((c0 * kChunk) >> 6) * a.lda + asset];
@@ -1124,7 +1202,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     LDS Smem& sm = *smp;
     // this lane's byte offset inside a date row: every output / mask store is an SGPR row base
     // plus this offset (no 64-bit per-lane address kept live through the scan)
-    const uint32_t voff = (uint32_t)((block * kLanes + lane) * 8);
+    const uint32_t voff = (uint32_t)((block * kLanes + lane_asset(lane)) * 8);
     const int c0 = a.c0, nch = a.c1;
     const int64_t w0 = ((int64_t)c0 * kChunk) >> 6;                     // the slab's first word
     constexpr unsigned S = P::kSer;
@@ -1159,6 +1237,8 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     st.rn = &rn;
     st.plane = a.plane;
     st.voff = voff;
+    st.poff = (uint32_t)((block * kLanes + 2 * (lane & 31)) * 8);
+    st.hmask = lane >= 32 ? -1 : 0;
     st.lane = lane;
     // The steps of chunk ch over its present days, on one of the three paths (uniform in the wave).
     auto fast_chunk = [&](int ch, unsigned cb, unsigned& n8, unsigned& f8) {
@@ -1166,8 +1246,9 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
         int p = pos, pm = pmod;
 #pragma unroll 1
         for (int s = 0; s < kChunk; ++s, row += a.lda) {
-            if (cb & (1u << s)) {
-                st.out = row;
+            const bool pres = (cb >> s) & 1u;
+            st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
+            if (pres) {
                 st.p = p;
                 st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
                 st.anynan = false;
@@ -1193,6 +1274,10 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                 ++p;
                 pm = pm + 1 == kRing ? 0 : pm + 1;
             }
+            if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
+                st.out = row;
+                st.template flush<P::kOut.lo, P::kOut.hi>();
+            }
         }
         pos = p;
         pmod = pm;
@@ -1207,8 +1292,9 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
             // p = 57 the lane is clean and the fast columns' own tracking applies.
 #pragma unroll 1
             for (int s = 0; s < kChunk; ++s, row += a.lda) {
-                if (cb & (1u << s)) {
-                    st.out = row;
+                const bool pres = (cb >> s) & 1u;
+                st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
+                if (pres) {
                     st.p = p;
                     st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
                     st.gather();
@@ -1236,12 +1322,17 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                     ++p;
                     pm = pm + 1 == kRing ? 0 : pm + 1;
                 }
+                if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
+                    st.out = row;
+                    st.template flush<P::kOut.lo, P::kOut.hi>();
+                }
             }
         } else {
 #pragma unroll 1
             for (int s = 0; s < kChunk; ++s, row += a.lda) {
-                if (cb & (1u << s)) {
-                    st.out = row;
+                const bool pres = (cb >> s) & 1u;
+                st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
+                if (pres) {
                     st.p = p;
                     st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
                     st.anynan = false;
@@ -1271,6 +1362,10 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                     f8 |= st.anybad ? 1u << s : 0u;
                     ++p;
                     pm = pm + 1 == kRing ? 0 : pm + 1;
+                }
+                if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
+                    st.out = row;
+                    st.template flush<P::kOut.lo, P::kOut.hi>();
                 }
             }
         }

@@ -1480,55 +1480,82 @@ constexpr int kRec = 4 + 2 * kMaxTerms + kMaxLevels;   // record words (fixed gl
 //         [4, 4+m) term codes (3 * prev side + new side; side 2 = absent),
 //         [4+m, 4+m+nint) adds in level order: left | right << 16 (node ids: terms 0..m-1,
 //         add q -> m + q), then L cumulative add counts per level.
-struct Dag {
-    int m, nint;
-    int l[kMaxTerms], r[kMaxTerms];
-    int lev[2 * kMaxTerms];
+// The full summation tree of numpy's pairwise_sum over n slots (numpy/_core/src/umath/
+// loops_utils.h.src): a node of more than 128 slots adds its halves (n2 = n / 2 rounded down to a
+// multiple of 8); a block of 8 <= n <= 128 slots runs 8 strided accumulators (chains, a[j] then
+// += a[j + 8c]), combines them ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) and adds the
+// n % 8 tail slots one by one; a block of n < 8 slots adds them one by one onto 0.  Restricted to
+// the member terms, the DAG's adds are exactly the lowest common ancestors of the terms that are
+// consecutive in the tree's in-order, so it is the Cartesian tree of those ancestors' depths --
+// built here lane-parallel (round 4; a one-lane recursive build took ~200 us per date).
+// Buffered reduction over more than 8192 slots: np_key / np_lca_depth below.
+struct PwBlock {
+    int64_t lo, len;
+    int depth;
 };
-
-__device__ int dag_add(Dag& d, int a, int b) {
-    if (a < 0) return b;
-    if (b < 0) return a;
-    const int id = d.m + d.nint;
-    d.l[d.nint] = a;
-    d.r[d.nint] = b;
-    d.lev[id] = (d.lev[a] > d.lev[b] ? d.lev[a] : d.lev[b]) + 1;
-    d.nint++;
-    return id;
-}
-
-// symbolic numpy pairwise_sum over positions [lo, lo + n) restricted to the terms [b, e) (sorted
-// by position): returns the node holding the subtree's sum, -1 if the subtree has no term
-__device__ int build_dag(Dag& d, const int* pos, int64_t lo, int64_t n, int b, int e) {
-    while (b < e && pos[b] < lo) ++b;
-    int ee = b;
-    while (ee < e && pos[ee] < lo + n) ++ee;
-    if (ee == b) return -1;
-    if (n <= 128) {
-        if (n < 8) {                                       // res = 0.; res += a[i]
-            int acc = -1;
-            for (int q = b; q < ee; ++q) acc = dag_add(d, acc, q);
-            return acc;
-        }
-        const int64_t body = n - (n % 8);                  // 8 strided accumulators, then tail
-        int r[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
-        for (int q = b; q < ee; ++q) {
-            const int64_t off = pos[q] - lo;
-            if (off < body) r[off % 8] = dag_add(d, r[off % 8], q);
-        }
-        const int r01 = dag_add(d, r[0], r[1]), r23 = dag_add(d, r[2], r[3]);
-        const int r45 = dag_add(d, r[4], r[5]), r67 = dag_add(d, r[6], r[7]);
-        const int lo4 = dag_add(d, r01, r23), hi4 = dag_add(d, r45, r67);
-        int res = dag_add(d, lo4, hi4);
-        for (int q = b; q < ee; ++q)
-            if (pos[q] - lo >= body) res = dag_add(d, res, q);
-        return res;
+__device__ __forceinline__ PwBlock pw_block(int64_t n, int64_t pos) {
+    int64_t lo = 0, len = n;
+    int d = 0;
+    while (len > 128) {
+        int64_t n2 = len / 2;
+        n2 -= n2 % 8;
+        if (pos < lo + n2) len = n2;
+        else { lo += n2; len -= n2; }
+        ++d;
     }
-    int64_t n2 = n / 2;
-    n2 -= n2 % 8;
-    const int L = build_dag(d, pos, lo, n2, b, ee);
-    const int R = build_dag(d, pos, lo + n2, n - n2, b, ee);
-    return dag_add(d, L, R);
+    return {lo, len, d};
+}
+// the in-order key of a slot inside its block: accumulator-major in the body, then the tail
+__device__ __forceinline__ int pw_inkey(const PwBlock& b, int64_t pos) {
+    const int off = (int)(pos - b.lo);
+    if (b.len < 8) return off;
+    const int body = (int)(b.len - b.len % 8);
+    return off < body ? (off % 8) * 16 + off / 8 : 128 + (off - body);
+}
+// depth (root 0) of the lowest common ancestor of the slots p and q, p before q in in-order
+__device__ int pw_lca_depth(int64_t n, int64_t p, int64_t q);
+// np.add.reduce over n slots (what Series.sum runs): the identity 0.0, then the pairwise sums of
+// consecutive 8192-slot buffers (NPY_BUFSIZE) added one by one -- over 8192 slots the sum is NOT
+// one pairwise tree (config C's id unions are ~9,000-10,000 long; oracle np_sum, checked against
+// numpy itself in tests/test_oracle_golden.py).  The full tree: a left-deep chain over the
+// buffers (buffer c joins at depth K - 1 - c), buffer c's pairwise tree rooted at depth K - c
+// (buffer 0: K, below the add of the identity).
+constexpr int64_t kNpBuf = 8192;
+__device__ __forceinline__ int np_key(int64_t n, int64_t pos) {
+    const int64_t c0 = pos - pos % kNpBuf;
+    const int64_t cl = n - c0 < kNpBuf ? n - c0 : kNpBuf;
+    const PwBlock b = pw_block(cl, pos - c0);
+    return (int)((c0 + b.lo) << 8) | pw_inkey(b, pos - c0);
+}
+__device__ int np_lca_depth(int64_t n, int64_t p, int64_t q) {
+    const int K = (int)((n + kNpBuf - 1) / kNpBuf);
+    const int cp = (int)(p / kNpBuf), cq = (int)(q / kNpBuf);
+    if (cp != cq) return K - 1 - cq;
+    const int64_t c0 = (int64_t)cq * kNpBuf;
+    const int64_t cl = n - c0 < kNpBuf ? n - c0 : kNpBuf;
+    return (cq == 0 ? K : K - cq) + pw_lca_depth(cl, p - c0, q - c0);
+}
+__device__ int pw_lca_depth(int64_t n, int64_t p, int64_t q) {
+    int64_t lo = 0, len = n;
+    int d = 0;
+    while (len > 128) {
+        int64_t n2 = len / 2;
+        n2 -= n2 % 8;
+        const bool lp = p < lo + n2, lq = q < lo + n2;
+        if (lp != lq) return d;
+        if (lp) len = n2;
+        else { lo += n2; len -= n2; }
+        ++d;
+    }
+    const int op = (int)(p - lo), oq = (int)(q - lo), nb = (int)len;
+    if (nb < 8) return d + (nb - 1 - oq);               // the add of slot q onto the running sum
+    const int nt = nb % 8, body = nb - nt;
+    if (oq >= body) return d + (nt - 1 - (oq - body));  // q's tail add
+    const int jp = op % 8, jq = oq % 8;
+    if (jp == jq) return d + nt + 3 + (body / 8 - 1 - oq / 8);   // q's add in its chain
+    if (jp / 2 == jq / 2) return d + nt + 2;
+    if (jp / 4 == jq / 4) return d + nt + 1;
+    return d + nt;
 }
 
 // Steps i are grouped in sequences of `seq` (one bootstrap path each; seq = nd for the plain
@@ -1540,9 +1567,9 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
                                                             const int64_t* usize, int32_t* rec,
                                                             int32_t* rlen, const int32_t* idx,
                                                             int64_t seq) {
-    __shared__ Dag dag;
     __shared__ int pos_s[kMaxTerms], code_s[kMaxTerms], pos_o[kMaxTerms], code_o[kMaxTerms];
-    __shared__ int newid[kMaxTerms], lcount[kMaxLevels + 1];
+    __shared__ int key_s[kMaxTerms], dep[kMaxTerms], lch[kMaxTerms], rch[kMaxTerms];
+    __shared__ int hgt[kMaxTerms], newid[kMaxTerms], lcount[kMaxLevels + 1];
     __shared__ int cnt, nlev;
     const int64_t i = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1584,51 +1611,106 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
     }
     __syncthreads();
     const int m = cnt;
-    for (int e = tid; e < m; e += 64) {              // sort by union position (distinct)
+    const int64_t n = usize[i * 2 + 0];
+    for (int e = tid; e < m; e += 64) key_s[e] = np_key(n, pos_s[e]);   // the tree's in-order
+    __syncthreads();
+    for (int e = tid; e < m; e += 64) {
         int r = 0;
-        for (int f = 0; f < m; ++f) r += pos_s[f] < pos_s[e];
+        for (int f = 0; f < m; ++f) r += key_s[f] < key_s[e];
         pos_o[r] = pos_s[e];
         code_o[r] = code_s[e];
     }
     __syncthreads();
-    if (tid == 0) {
-        dag.m = m;
-        dag.nint = 0;
-        for (int q = 0; q < m; ++q) dag.lev[q] = 0;
-        int L = 0;
-        if (m > 0) {
-            const int root = build_dag(dag, pos_o, 0, usize[i * 2 + 0], 0, m);
-            L = dag.lev[root];
-        }
-        nlev = L;
-        for (int l = 0; l <= L; ++l) lcount[l] = 0;
-        for (int q = 0; q < dag.nint; ++q) lcount[dag.lev[m + q]]++;
-        int acc = 0;                                  // lcount[l] -> first slot of level l
-        for (int l = 1; l <= L; ++l) { const int c = lcount[l]; lcount[l] = acc; acc += c; }
-        for (int q = 0; q < dag.nint; ++q) newid[q] = lcount[dag.lev[m + q]]++;
-        R[0] = active ? m : -1;
-        R[1] = dag.nint;
-        R[2] = L;
-        R[3] = 0;
-        rlen[i] = 4 + (active ? m : 0) + dag.nint + L;
+    // internal node k (0 <= k < m - 1) = the LCA of in-order terms k and k + 1
+    const int ni = m > 1 ? m - 1 : 0;
+    for (int k = tid; k < ni; k += 64) dep[k] = np_lca_depth(n, pos_o[k], pos_o[k + 1]);
+    __syncthreads();
+    // Cartesian tree: the left child of k is the shallowest node between the nearest shallower
+    // node on its left and k (or term k), the right child likewise (or term k + 1); child ids:
+    // term t -> t, node k -> m + k
+    for (int k = tid; k < ni; k += 64) {
+        const int dk = dep[k];
+        int best = -1, bd = 1 << 30;
+        for (int l = k - 1; l >= 0 && dep[l] > dk; --l)
+            if (dep[l] < bd) { bd = dep[l]; best = l; }
+        lch[k] = best < 0 ? k : m + best;
+        best = -1;
+        bd = 1 << 30;
+        for (int r = k + 1; r < ni && dep[r] > dk; ++r)
+            if (dep[r] < bd) { bd = dep[r]; best = r; }
+        rch[k] = best < 0 ? k + 1 : m + best;
+        hgt[k] = 1;
     }
     __syncthreads();
-    const int nint = dag.nint, L = nlev;
+    // heights (the DAG level of an add: 1 + its children's), relaxed until they settle
+    for (int it = 0; it < kMaxLevels + 1; ++it) {
+        bool ch = false;
+        for (int k = tid; k < ni; k += 64) {
+            const int a = lch[k], b = rch[k];
+            const int ha = a < m ? 0 : hgt[a - m], hb = b < m ? 0 : hgt[b - m];
+            const int h = (ha > hb ? ha : hb) + 1;
+            if (h != hgt[k]) { hgt[k] = h; ch = true; }
+        }
+        __syncthreads();
+        if (__syncthreads_or(ch) == 0) break;
+    }
+    if (tid <= kMaxLevels) lcount[tid] = 0;
+    if (tid == 0) nlev = 0;
+    __syncthreads();
+    for (int k = tid; k < ni; k += 64) {
+        atomicAdd(&lcount[hgt[k]], 1);
+        atomicMax(&nlev, hgt[k]);
+    }
+    __syncthreads();
+    const int L = nlev;
+    if (tid == 0) {
+        int acc = 0;                                  // lcount[l] -> first slot of level l
+        for (int l = 1; l <= L; ++l) { const int c = lcount[l]; lcount[l] = acc; acc += c; }
+        R[0] = active ? m : -1;
+        R[1] = ni;
+        R[2] = L;
+        R[3] = 0;
+        rlen[i] = 4 + (active ? m : 0) + ni + L;
+    }
+    __syncthreads();
+    for (int k = tid; k < ni; k += 64) newid[k] = atomicAdd(&lcount[hgt[k]], 1);
+    __syncthreads();
     for (int e = tid; e < m; e += 64) R[4 + e] = code_o[e];
-    for (int q = tid; q < nint; q += 64) {
-        const int a = dag.l[q], b = dag.r[q];
+    for (int k = tid; k < ni; k += 64) {
+        const int a = lch[k], b = rch[k];
         const int na = a < m ? a : m + newid[a - m];
         const int nb = b < m ? b : m + newid[b - m];
-        R[4 + m + newid[q]] = na | (nb << 16);
+        R[4 + m + newid[k]] = na | (nb << 16);
     }
-    for (int l = tid; l < L; l += 64) R[4 + m + nint + l] = lcount[l + 1];   // cumulative ends
+    for (int l = tid; l < L; l += 64) R[4 + m + ni + l] = lcount[l + 1];   // cumulative ends
 }
 
 constexpr int kChunkDates = 64;
 constexpr int kBufWords = 12288;
 
-// One workgroup of 2 waves.  Wave 1 stages chunk c+1 (records + sums) into LDS while wave 0
-// runs chunk c; one barrier per chunk.  Wave 0 keeps V / V_prev replicated in every lane.
+// x / d from r = RN(1 / d) (Markstein: q0 = RN(x r), e = fma(-q0, d, x), q = RN(q0 + e r) is the
+// IEEE quotient when r is the correctly rounded reciprocal and nothing under- or overflows; the
+// same correction as lasso.hip div_r).  Out of that range (or d = 0, inf, NaN) the IEEE division.
+__device__ __forceinline__ double mdiv(double x, double d, double r) {
+    const double q0 = x * r;
+    const double e = __builtin_fma(-q0, d, x);
+    const double q1 = __builtin_fma(e, r, q0);
+    const double aq = __builtin_fabs(q0), ar = __builtin_fabs(r);
+    const bool ok = aq > 0x1p-400 && aq < 0x1p400 && ar > 0x1p-400 && ar < 0x1p400;
+    if (__builtin_expect(!ok, 0)) return x / d;
+    return q1;
+}
+
+// One workgroup of 2 waves.  Wave 1 stages chunk c+1 (records, sums and the reciprocals of the
+// two price sums) into LDS while wave 0 runs chunk c; one barrier per chunk.  Wave 0 keeps V /
+// V_prev replicated in every lane; its per-date chain (round 4: 1.95 -> ~0.5 us per date) is
+//   V -> share counts (Markstein quotients on the staged reciprocals, 3 dependent ops each)
+//     -> the |c - n| leaves -> the DAG levels of the turnover sum -> turnover cost / V
+//     (Markstein on RN(1 / V), computed beside the tree) -> V (1 + daily);
+// every V-independent read of date j + 1 (record header, leaf codes, sums, reciprocals, the
+// first level's add descriptor) is issued during date j, and the DAG levels run without
+// lgkmcnt(0) waits: only this wave touches node[], and one wave's LDS operations execute in
+// order, so a level's reads see the previous level's writes.
 // Workgroup b scans the steps [b * nd, (b + 1) * nd) (bootstrap path b; one workgroup for the
 // plain sequence); the sums of step i are those of book slot ix(i).
 __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double* sums,
@@ -1639,6 +1721,7 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
     __shared__ int buf[2][kBufWords];
     __shared__ int offs[2][kChunkDates];
     __shared__ double sm[2][kChunkDates + 1][4];
+    __shared__ double rcp[2][kChunkDates + 1][2];           // RN(1 / S[2]), RN(1 / S[3])
     __shared__ int64_t cstart[2];
     __shared__ int ccount[2];
     __shared__ double node[2 * kMaxTerms];
@@ -1672,7 +1755,9 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
         }
         for (int e = lane; e < (c + 1) * 4; e += 64) {
             const int64_t ii = i0 - 1 + e / 4;
-            sm[b][e / 4][e % 4] = ii >= 0 ? sums[(idx ? (int64_t)idx[ii] : ii) * 4 + e % 4] : 0.0;
+            const double v = ii >= 0 ? sums[(idx ? (int64_t)idx[ii] : ii) * 4 + e % 4] : 0.0;
+            sm[b][e / 4][e % 4] = v;
+            if (e % 4 >= 2) rcp[b][e / 4][e % 4 - 2] = 1.0 / v;
         }
         if (lane == 0) { cstart[b] = i0; ccount[b] = c; }
         return i0 + c;
@@ -1695,32 +1780,57 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
             else if (lane == 0) ccount[b ^ 1] = 0;
         } else {
             const int64_t i0 = cstart[b];
-            for (int j = 0; j < c; ++j) {
-                const int* R = &buf[b][offs[b][j]];
+            // date j's V-independent inputs, read one date ahead
+            struct Pre {
+                const int* R;
+                int m, nint, L, code, en0, w0;
+                double s0, s1, s2, s3, r2, r3;
+            };
+            auto prefetch = [&](int j) {
+                Pre f;
+                f.R = &buf[b][offs[b][j]];
+                f.m = f.R[0];
+                f.nint = f.R[1];
+                f.L = f.R[2];
                 const double* S = sm[b][j + 1];
-                const int m = R[0];
+                f.s0 = S[0]; f.s1 = S[1]; f.s2 = S[2]; f.s3 = S[3];
+                f.r2 = rcp[b][j + 1][0];
+                f.r3 = rcp[b][j + 1][1];
+                f.code = lane < f.m ? f.R[4 + lane] : 0;
+                const int* lend = f.R + 4 + (f.m > 0 ? f.m : 0) + f.nint;
+                f.en0 = f.m > 0 && f.L > 0 ? lend[0] : 0;
+                f.w0 = lane < f.en0 ? f.R[4 + f.m + lane] : 0;
+                return f;
+            };
+            Pre cur = prefetch(0);
+            for (int j = 0; j < c; ++j) {
+                const Pre f = cur;
+                if (j + 1 < c) cur = prefetch(j + 1);
+                const int m = f.m;
                 double to = 0.0;
                 const double size = V / 2;
-                const double qc = size / S[2], qd = size / S[3];      // today's share counts
+                const double qc = mdiv(size, f.s2, f.r2), qd = mdiv(size, f.s3, f.r3);
+                const double rv = 1.0 / V;                             // beside the tree
                 if (m > 0) {
-                    const int nint = R[1], L = R[2];
-                    for (int e = lane; e < m; e += 64) {              // term values |c - n|
-                        const int sd = R[4 + e];
+                    const int* R = f.R;
+                    const int nint = f.nint, L = f.L;
+                    auto leaf = [&](int sd) {
                         const int ps = sd / 3, ns = sd % 3;
                         // (-x) / y == -(x / y) exactly: the reference's -size / sum
                         const double cv = ps == 0 ? qa : (ps == 1 ? -qb : 0.0);
                         const double nv = ns == 0 ? qc : (ns == 1 ? -qd : 0.0);
                         const double d = cv - nv;
-                        node[e] = d < 0 ? -d : d;
-                    }
-                    lds_sync();
+                        return d < 0 ? -d : d;
+                    };
+                    if (lane < m) node[lane] = leaf(f.code);
+                    for (int e = lane + 64; e < m; e += 64) node[e] = leaf(R[4 + e]);
                     const int* adds = R + 4 + m;
                     const int* lend = adds + nint;
-                    // one DAG level per step; the next level's first add descriptor is fetched
-                    // while this level's node reads are in flight (descriptors are value-free)
+                    // one DAG level per step, no lgkmcnt(0) wait (see above); the next level's
+                    // first add descriptor is fetched while this level's node reads are in flight
                     int st = 0;
-                    int en = L > 0 ? lend[0] : 0;
-                    int wcur = lane < en ? adds[lane] : 0;
+                    int en = f.en0;
+                    int wcur = f.w0;
                     for (int l = 0; l < L; ++l) {
                         const int en2 = l + 1 < L ? lend[l + 1] : en;
                         const int wnext = en + lane < en2 ? adds[en + lane] : 0;
@@ -1731,24 +1841,22 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                         st = en;
                         en = en2;
                         wcur = wnext;
-                        lds_sync();
                     }
                     to = node[nint > 0 ? m + nint - 1 : 0] / 2;
                 }
-                double daily = (S[0] - S[1]) / 2;
-                daily -= (to * rate) / V;
+                double daily = (f.s0 - f.s1) / 2;
+                daily -= mdiv(to * rate, V, rv);
                 const double Vn = V * (1 + daily);
                 if (lane == 0) {
                     const int64_t i = i0 + j;
-                    long_ret[i] = S[0];
-                    short_ret[i] = S[1];
+                    long_ret[i] = f.s0;
+                    short_ret[i] = f.s1;
                     turnover[i] = to;
                     value[i + 1] = Vn;
                 }
                 qa = qc;
                 qb = qd;
                 V = Vn;
-                lds_sync();                                           // node[] reused next date
             }
         }
         __syncthreads();

@@ -176,6 +176,8 @@ def main():
     ap.add_argument("--days", type=int, default=5040)
     ap.add_argument("--seed", type=int, default=2023)
     ap.add_argument("--top-n", type=int, default=10)
+    ap.add_argument("--fm-free-cus", type=int, default=None,
+                    help="PipelineConfig.fm_free_cus (CUs the FM side stream leaves free)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the top_n_100 / dense_lasso secondary lines (N = 1 only)")
@@ -209,6 +211,8 @@ def main():
     del p
     n_ad = grid.n_asset_days()                         # the whole panel (strong scaling)
     cfg = PipelineConfig(top_n=args.top_n)
+    if args.fm_free_cus is not None:
+        cfg = PipelineConfig(top_n=args.top_n, fm_free_cus=args.fm_free_cus)
     if world > 1:
         from afm.sharded import EXCHANGE_STAGES, Comm, ShardedPipeline
         pipe = ShardedPipeline(grid, Comm(), cfg)

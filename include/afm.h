@@ -47,6 +47,14 @@ int afm_ctx_set_stream(afm_ctx* ctx, void* stream);
  *   "factor_fast"   1 (default) | 0: the clean-window fast step of the factor kernel
  *   "gram_checked"  0 (default) | 1: afm_xs_gram_f64 stages every row checked (no FAST + REDO) */
 int afm_ctx_set_option(afm_ctx* ctx, const char* name, int64_t value);
+/* The current value of an option of afm_ctx_set_option (value: out). */
+int afm_ctx_get_option(afm_ctx* ctx, const char* name, int64_t* value);
+/* A stream whose kernels run only on the compute units set in cu_mask (nwords 32-bit words, bit i
+ * = the i-th compute unit of the device's logical CU mask; hipExtStreamCreateWithCUMask); the
+ * pipeline places its FM per-date Grams on one so latency-bound kernels keep whole CUs.  *out:
+ * the hipStream_t.  afm_stream_destroy releases it. */
+int afm_stream_create_cu_mask(int device, const uint32_t* cu_mask, int nwords, void** out);
+int afm_stream_destroy(void* stream);
 int afm_ctx_destroy(afm_ctx* ctx);
 const char* afm_last_error(void);
 int afm_version(void);

@@ -34,8 +34,15 @@ static double pairwise(const double* a, int64_t n) {
     }
 }
 
-/* np.add.reduce: identity 0.0 then the pairwise sum of the whole contiguous vector */
-double oracle_np_sum(int64_t n, const double* a) { return 0.0 + pairwise(a, n); }
+/* np.add.reduce on a contiguous float64 vector: the identity 0.0, then the pairwise sums of the
+ * consecutive 8192-element buffers of the ufunc's buffered reduction (NPY_BUFSIZE) added one by
+ * one -- a vector over 8192 elements is NOT one pairwise tree (tests/test_oracle_golden.py checks
+ * this against numpy itself, up to 40,000 elements) */
+double oracle_np_sum(int64_t n, const double* a) {
+    double res = 0.0;
+    for (int64_t i = 0; i < n; i += 8192) res += pairwise(a + i, n - i < 8192 ? n - i : 8192);
+    return res;
+}
 
 /* nancorr for one pair (xi = the LATER column, yi = the earlier one), minp = 1 */
 double oracle_nancorr_pair(int64_t n, const double* vxcol, const double* vycol) {

@@ -121,3 +121,19 @@ def test_zscore_and_ols(golden_dir):
     assert a1 == o["sub_intercept"][0] and same(c1, o["sub_coef"])
     a0, c0 = PL.pooled_ols(Xtr, ytr)
     assert abs(a0 - o["full_intercept"][0]) < 1e-6 and np.abs(c0 - o["full_coef"]).max() < 1e-6
+
+
+def test_np_sum_matches_numpy_buffered_reduce():
+    """oracle np_sum = numpy's own np.add.reduce (pandas Series.sum / mean, KKT:315-318, the
+    turnover sum of KKT:887) -- including vectors longer than numpy's 8192-element reduction
+    buffer, where the result is NOT one pairwise tree (the per-date groups and id unions of the
+    10,000-asset config are ~9,000-10,000 long)."""
+    from oracle.xs import np_sum
+    rng = np.random.default_rng(12)
+    for n in [0, 1, 7, 8, 127, 128, 129, 1000, 8191, 8192, 8193, 9000, 16384, 16385, 24577,
+              40000]:
+        for scale in (1.0, 1e-3, 1e8):
+            v = rng.standard_normal(n) * scale * 10.0 ** rng.integers(-2, 3, n)
+            assert np_sum(v) == np.sum(v), (n, scale)
+            sparse = np.where(rng.random(n) < 0.004, np.abs(v), 0.0)   # a turnover vector
+            assert np_sum(sparse) == np.sum(sparse), (n, scale)

@@ -253,3 +253,79 @@ def test_top100_books_weights_pnl_vs_oracle():
         assert np.abs(pm.weights[j, 1, :top_n] - wos).max() < 1e-9
     v = np.asarray(pm.portfolio_value["Portfolio"], dtype=np.float64)
     assert np.abs(v - o["value"]).max() / o["value"].max() < 1e-12
+
+
+@pytest.mark.parametrize("A", [9800])
+def test_large_union_turnover_vs_numpy_reduce(A):
+    """Prediction-id unions of ~9,800 names (config C scale): numpy's np.add.reduce sums over its
+    8192-element buffers one by one, so the turnover sum (Series.sum, KKT:887) is not one pairwise
+    tree.  The engine's turnover DAG (np_lca_depth) and the oracle (np_sum, pinned to numpy) must
+    agree bit for bit on turnover and value."""
+    from afm.portfolio import PortfolioManager
+    from oracle import portfolio as P
+    rng = np.random.default_rng(A)
+    T, top_n = 112, 10
+    dates = np.asarray(np.busday_offset(np.datetime64("2016-01-04"), np.arange(T), roll="forward"),
+                       dtype="datetime64[ns]")
+    ids = 5 + 2 * np.arange(A)
+    present = rng.random((T, A)) < 0.97
+    tt, aa = np.nonzero(present)
+    d, i = dates[tt], ids[aa]
+    ret = rng.normal(0, 0.02, len(tt))
+    close = 50 * np.exp(rng.normal(0, 0.1, len(tt)))
+    trad = rng.random(len(tt)) < 0.9
+    hist_m = tt < 100
+    test_m = tt >= 100
+    pred_v = rng.normal(size=test_m.sum())
+    pred = pd.DataFrame({"p": pred_v}, index=pd.MultiIndex.from_arrays([d[test_m], i[test_m]]))
+    hist = pd.DataFrame({"target": ret[hist_m]}, index=pd.MultiIndex.from_arrays([d[hist_m], i[hist_m]]))
+    all_df = pd.DataFrame({"in_trading_universe": np.where(trad, "Y", "N"), "close_price": close,
+                           "tmr_ret1d": ret}, index=pd.MultiIndex.from_arrays([d, i]))
+    pm = PortfolioManager(pred, hist, all_df, top_n=top_n, window=60)
+    pm.calculate_portfolio()
+    o = P.run_portfolio(d[test_m].astype(np.int64), i[test_m], pred_v,
+                        d[hist_m].astype(np.int64), i[hist_m], ret[hist_m],
+                        d.astype(np.int64), i, trad, close, ret, top_n=top_n, window=60)
+    for (dt, L, S), Lo, So in zip(pm.books, o["books"][0::2], o["books"][1::2]):
+        assert L == Lo.tolist() and S == So.tolist()
+    assert same(np.asarray(pm.turnovers, dtype=np.float64), o["turnover"])
+    assert same(np.asarray(pm.portfolio_value["Portfolio"], dtype=np.float64), o["value"])
+
+
+def test_large_book_full_history_window_vs_oracle():
+    """Books over 32 names with no rolling window (the reference's whole training history,
+    KKT:858-859) whose history starts after the first grid date: the member-major history panel
+    is staged from that later start."""
+    from afm.portfolio import PortfolioManager
+    from oracle import portfolio as P
+    rng = np.random.default_rng(41)
+    T, A, top_n = 150, 160, 40
+    dates = np.asarray(np.busday_offset(np.datetime64("2016-01-04"), np.arange(T), roll="forward"),
+                       dtype="datetime64[ns]")
+    ids = 3 + 7 * np.arange(A)
+    present = rng.random((T, A)) < 0.96
+    tt, aa = np.nonzero(present)
+    d, i = dates[tt], ids[aa]
+    f = rng.normal(0, 0.01, (T, 3))
+    ret = (f @ rng.normal(0, 1, (3, A)))[tt, aa] + rng.normal(0, 0.02, len(tt))
+    close = 50 * np.exp(rng.normal(0, 0.1, len(tt)))
+    trad = rng.random(len(tt)) < 0.95
+    hist_m = (tt >= 23) & (tt < 130)                    # history from grid date 23 on
+    test_m = tt >= 130
+    pred_v = rng.normal(size=test_m.sum())
+    pred = pd.DataFrame({"p": pred_v}, index=pd.MultiIndex.from_arrays([d[test_m], i[test_m]]))
+    hist = pd.DataFrame({"target": ret[hist_m]}, index=pd.MultiIndex.from_arrays([d[hist_m], i[hist_m]]))
+    all_df = pd.DataFrame({"in_trading_universe": np.where(trad, "Y", "N"), "close_price": close,
+                           "tmr_ret1d": ret}, index=pd.MultiIndex.from_arrays([d, i]))
+    pm = PortfolioManager(pred, hist, all_df, top_n=top_n, window=None)
+    pm.calculate_portfolio()
+    o = P.run_portfolio(d[test_m].astype(np.int64), i[test_m], pred_v,
+                        d[hist_m].astype(np.int64), i[hist_m], ret[hist_m],
+                        d.astype(np.int64), i, trad, close, ret, top_n=top_n, window=None)
+    for (dt, L, S), Lo, So in zip(pm.books, o["books"][0::2], o["books"][1::2]):
+        assert L == Lo.tolist() and S == So.tolist()
+    for j, (wol, wos) in enumerate(zip(o["weights"][0::2], o["weights"][1::2])):
+        assert np.abs(pm.weights[j, 0, :top_n] - wol).max() < 1e-9
+        assert np.abs(pm.weights[j, 1, :top_n] - wos).max() < 1e-9
+    v = np.asarray(pm.portfolio_value["Portfolio"], dtype=np.float64)
+    assert np.abs(v - o["value"]).max() / o["value"].max() < 1e-12

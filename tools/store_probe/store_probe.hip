@@ -28,7 +28,20 @@ __global__ __launch_bounds__(768) void probe(double* out, const double* in, long
     const long plane = T * lda + pad;          // pad: extra doubles between consecutive planes
     double acc = 0.0;
     for (long ch = 0; ch * kChunk < T; ++ch) {
-        if (live && pos < 5 && (mode & 3) != 2 && (mode & 128)) {
+        if (live && pos < 5 && (mode & 3) != 2 && (mode & 64)) {
+            // +64: column-pair planes [48][T][lda][2]: one 16-B store per lane = two columns of
+            // one asset-day, 1 KB contiguous per instruction
+            typedef double dv2 __attribute__((ext_vector_type(2)));
+            for (int s = 0; s < kChunk; ++s) {
+                const long t = ch * kChunk + s;
+                if (t >= T) break;
+                for (int c = c0 & ~1; c < c1; c += 2) {
+                    const long off = (c >> 1) * 2 * plane + 2 * (t * lda + asset);
+                    const dv2 v = {(double)t, (double)c};
+                    *(dv2*)&out[off] = v;
+                }
+            }
+        } else if (live && pos < 5 && (mode & 3) != 2 && (mode & 128)) {
             // +128: 16-B stores, two columns per instruction (even lanes: column c of assets
             // 2i, 2i+1; odd lanes: column c + 1 of the same two assets)
             typedef double dv2 __attribute__((ext_vector_type(2)));
