@@ -1237,6 +1237,10 @@ __global__ __launch_bounds__(kT) void weights_kernel(const double* R, int64_t ro
         if (tid < k) sh.w[tid] = hi;
     } else if (k * lo >= 1.0) {
         if (tid < k) sh.w[tid] = lo;
+    } else if (k <= 32) {            // the solve rebalance_kernel<32> runs (headline books)
+        const bool ok = qp_setup(sh, k);
+        if (!ok) capped = true;
+        else if (tid < 64) capped = qp_wave(sh, k, lo, hi);
     } else {
         capped = qp_block(sh, k, lo, hi, nullptr);
     }
@@ -1942,13 +1946,22 @@ using namespace afm;
 
 // history rows [t0, t0 + n) of the [T][lda] panel -> member-major [lda][n], NaN where the
 // presence bit is clear (books over 32 names stage their windows from it, coalesced)
+// dates / window (window > 0): only the 64-date tiles that meet the rebalance dates' windows,
+// [dates[0] - window, dates[nd - 1] + 1), are copied (the dates ascend); the rest of hT is never
+// read (the whole panel was transposed on every call)
 __global__ __launch_bounds__(256) void hist_transpose_kernel(int64_t lda, int64_t A,
                                                              const double* hist,
                                                              const uint64_t* hbits, int64_t t0,
-                                                             int64_t n, double* hT) {
+                                                             int64_t n, double* hT,
+                                                             const int32_t* dates, int64_t nd,
+                                                             int64_t window) {
     __shared__ double tile[64][65];
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const int64_t tb = (int64_t)blockIdx.x * 64, ab = (int64_t)blockIdx.y * 64;
+    if (window > 0) {
+        const int64_t lo = (int64_t)dates[0] - window, hi = (int64_t)dates[nd - 1] + 1;
+        if (t0 + tb + 64 <= lo || t0 + tb >= hi) return;          // uniform: the whole tile
+    }
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int rr = w + 4 * j;
@@ -2013,7 +2026,8 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
                                    ctx->stream));
             hipLaunchKernelGGL(hist_transpose_kernel, dim3((unsigned)((hTn + 63) / 64),
                                                            (unsigned)(lda / 64)),
-                               dim3(256), 0, ctx->stream, lda, A, hist, hist_bits, hT0, hTn, histT);
+                               dim3(256), 0, ctx->stream, lda, A, hist, hist_bits, hT0, hTn, histT,
+                               dates, nd, window);
             AFM_HIP(hipGetLastError());
         }
     } else if (top_n * (top_n + 1) / 2 > kT && hrows > 0)
