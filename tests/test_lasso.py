@@ -111,3 +111,34 @@ def test_lasso_rejects_nonfinite():
     X[3, 1] = np.nan
     with pytest.raises(ValueError):
         afm.Lasso(alpha=0.1).fit(X, np.zeros(10))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p,alpha,pos", [(96, 2e-4, 0), (110, 5e-5, 0), (70, 1e-4, 1)])
+def test_kernel_dense_fit_bit_exact_vs_oracle(p, alpha, pos):
+    """Dense fits (many coefficients move every sweep, hundreds of sweeps, both column halves):
+    the kernel's pipelined coordinate step -- the next nonzero coordinate's row and H read while
+    the current one computes -- against the oracle's sequential descent, bit for bit."""
+    import torch
+    import oracle
+    from afm import _lib
+    rng = np.random.default_rng(p)
+    n = 4000
+    F = rng.normal(size=(n, 6))
+    X = F @ rng.normal(size=(6, p)) + 0.5 * rng.normal(size=(n, p))   # correlated columns
+    beta = np.where(rng.random(p) < 0.4, rng.normal(size=p), 0.0)
+    y = X @ beta + rng.normal(size=n)
+    Z = np.concatenate([np.ones((n, 1)), X, y[:, None]], 1)
+    G = torch.from_numpy(Z.T @ Z).cuda().contiguous()           # raw moments [1, x, y]
+    nn, Q, q, yy = oracle.centered_moments(G.cpu().numpy())
+    for tol in (1e-4, 1e-10):
+        w = torch.empty(p, dtype=torch.float64, device="cuda")
+        info = torch.empty(3, dtype=torch.float64, device="cuda")
+        h = _lib.Context.get(0).bind_stream()
+        _lib.check(_lib.lib().afm_lasso_cd_f64(h, _lib.ptr(G), p, alpha * n, 0.0, 10000, tol, pos,
+                                               _lib.ptr(w), _lib.ptr(info)))
+        wo, gap, tol_y, it = oracle.lasso_gram(Q, q, yy, alpha * nn, max_iter=10000, tol=tol,
+                                               positive=bool(pos))
+        assert (wo != 0).sum() >= 10 and it >= 5
+        assert np.array_equal(w.cpu().numpy(), wo)
+        assert info.cpu().numpy().tolist() == [gap, tol_y, float(it)]

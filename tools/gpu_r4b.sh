@@ -2,7 +2,7 @@
 # round 4: paired 16-B factor stores -- factor parity tests, then the kernel alone
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; o=gpurun_out/r4b; mkdir -p $o
-timeout -k 10 600 python -u -m pytest tests/test_factors_gpu.py tests/test_intraday_gpu.py tests/test_portfolio_gpu.py tests/test_chain_gpu.py tests/test_analyzer_gpu.py -x -q --timeout 200 --timeout-method thread > $o/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_factors_gpu.py tests/test_intraday_gpu.py tests/test_portfolio_gpu.py tests/test_chain_gpu.py tests/test_analyzer_gpu.py tests/test_lasso.py -x -q --timeout 200 --timeout-method thread > $o/tests.log 2>&1
 rc=$?; tail -5 $o/tests.log; [ $rc -eq 0 ] || exit 1
 for A in 10000 1250; do
   timeout -k 10 200 python -u tools/fp_probe.py --assets $A --reps 7 >> $o/fp.txt 2>&1 || exit 1
