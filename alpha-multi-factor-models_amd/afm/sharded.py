@@ -92,6 +92,40 @@ class Comm:
         self.dist.barrier(group=self.group)
 
 
+class EmulatedComm:
+    """One rank of a ``world``-rank job in a single process, for measuring what a rank computes
+    (``bench.py --emulate-world N``): every collective returns this rank's own contribution in
+    every other rank's slot, so the step runs exactly rank ``rank``'s kernels -- its asset shard,
+    its date shares -- on its own shapes, with no communication.  The results are not the
+    job's results (the other ranks' shares are copies); this is a timing device only."""
+
+    def __init__(self, world: int, rank: int = 0):
+        if world < 2 or not 0 <= rank < world:
+            raise ValueError("need world >= 2 and 0 <= rank < world")
+        self.world, self.rank, self.host = world, rank, False
+
+    def all_gather(self, t):
+        return t.contiguous().unsqueeze(0).expand((self.world,) + tuple(t.shape)).contiguous()
+
+    def all_gather_packed(self, tensors):
+        return [self.all_gather(t) for t in tensors]
+
+    def all_to_all(self, inp, in_splits, out_splits):
+        import torch
+        off = sum(in_splits[:self.rank])
+        own = inp[off:off + in_splits[self.rank]]
+        parts = []
+        for n in out_splits:                      # every sender's block: this rank's own rows
+            reps = -(-n // max(own.shape[0], 1))
+            parts.append(own.repeat((reps,) + (1,) * (own.dim() - 1))[:n] if own.shape[0]
+                         else torch.zeros((n,) + tuple(inp.shape[1:]), dtype=inp.dtype,
+                                          device=inp.device))
+        return torch.cat(parts)
+
+    def barrier(self):
+        pass
+
+
 def ShardedPipeline(grid: PanelGrid, comm: Comm, cfg: PipelineConfig | None = None) -> Pipeline:
     """``Pipeline.step()`` on one rank of ``comm.world`` (afm.pipeline.Pipeline with a comm):
     bit-identical to the single-device step for N in {1, 2, 4, 8}."""

@@ -178,6 +178,10 @@ def main():
     ap.add_argument("--top-n", type=int, default=10)
     ap.add_argument("--fm-free-cus", type=int, default=None,
                     help="PipelineConfig.fm_free_cus (CUs the FM side stream leaves free)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="time what ONE rank of an N-GPU job computes, on one GPU (collectives "
+                         "replaced by local copies, afm.sharded.EmulatedComm): a per-rank proxy, "
+                         "not a result of the job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the top_n_100 / dense_lasso secondary lines (N = 1 only)")
@@ -216,6 +220,11 @@ def main():
     if world > 1:
         from afm.sharded import EXCHANGE_STAGES, Comm, ShardedPipeline
         pipe = ShardedPipeline(grid, Comm(), cfg)
+        stages = EXCHANGE_STAGES
+        n_ad_local = pipe.n_asset_days_local()
+    elif args.emulate_world > 1:
+        from afm.sharded import EXCHANGE_STAGES, EmulatedComm
+        pipe = Pipeline(grid, cfg, EmulatedComm(args.emulate_world, 0))
         stages = EXCHANGE_STAGES
         n_ad_local = pipe.n_asset_days_local()
     else:
@@ -257,6 +266,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
 
+    if args.emulate_world > 1:          # per-rank proxy: no headline line
+        ms = elapsed / args.steps * 1e3
+        print(json.dumps({"emulated_world": args.emulate_world, "rank": 0,
+                          "assets_local": pipe.A_r, "ms_per_step": round(ms, 3),
+                          "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
+                          "note": "one rank's kernels on one GPU, collectives replaced by local "
+                                  "copies (afm.sharded.EmulatedComm); no communication time"}),
+              flush=True)
+        return
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         p2 = pipe.p2

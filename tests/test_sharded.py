@@ -235,3 +235,19 @@ def test_sharded_ranks_bit_identical_to_single(tmp_path, world):
                         rate=pipe.cfg.rate)
     assert np.array_equal(s["boot"], one["value"].cpu().numpy())
     assert np.array_equal(s["boot_to"], one["turnover"].cpu().numpy())
+
+
+def test_emulated_comm_shapes():
+    """EmulatedComm (bench.py --emulate-world): collectives return the right shapes with this
+    rank's share in every slot."""
+    import torch
+    from afm.sharded import EmulatedComm
+    c = EmulatedComm(4, 1)
+    t = torch.arange(6.0).view(2, 3)
+    g = c.all_gather(t)
+    assert g.shape == (4, 2, 3) and all(torch.equal(g[q], t) for q in range(4))
+    a, b = c.all_gather_packed([t, torch.ones(5, dtype=torch.int32)])
+    assert a.shape == (4, 2, 3) and b.shape == (4, 5) and b.dtype == torch.int32
+    inp = torch.arange(10.0).view(10, 1)                   # rank 1 owns rows [3, 6)
+    out = c.all_to_all(inp, [3, 3, 2, 2], [3, 3, 3, 3])
+    assert out.shape == (12, 1) and torch.equal(out[3:6], inp[3:6])

@@ -12,3 +12,7 @@ for f in 0 16 32 64; do
   timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-variants --fm-free-cus $f > $o/bench_fm$f.json 2> $o/bench_fm$f.err || { tail -5 $o/bench_fm$f.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('$o/bench_fm$f.json')); print('fm_free_cus $f', d['ms_per_step'], d['stage_ms'])"
 done
+for W in 8 4 2; do
+  timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --emulate-world $W > $o/emu$W.json 2> $o/emu$W.err || { tail -5 $o/emu$W.err; exit 1; }
+  cat $o/emu$W.json
+done
