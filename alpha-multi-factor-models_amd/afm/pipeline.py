@@ -355,9 +355,13 @@ class Pipeline:
             raise ValueError(f"fm_fork={c.fm_fork!r}: expected gram, predict, analyzer or "
                              "rebalance")
         self.main = torch.cuda.Stream(device=dev, priority=-8 if c.main_priority else 0)
+        self.fm_grid = 0                  # the FM Grams' persistent grid (0: one per CU)
         if c.fm_free_cus > 0:
             self._side_owner = _lib.cu_mask_stream(dev.index, c.fm_free_cus)
             self.side = self._side_owner.stream
+            # one workgroup per CU the masked stream may use: a full-width grid would run the
+            # surplus workgroups in a second round
+            self.fm_grid = torch.cuda.get_device_properties(dev).multi_processor_count - c.fm_free_cus
         else:
             self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
@@ -408,7 +412,7 @@ class Pipeline:
             return
         chk(L.afm_zgram_f64(h, P(self.out), T * lda, lda, P(self.fm_cols), None, pf, TARGET,
                             None, 0, P(self.zrows), 0, T, self.nblk_r, 0, self.blk, self.A_r,
-                            P(self.fm_part), 0), "zgram fm")
+                            P(self.fm_part), self.fm_grid), "zgram fm")
         chk(L.afm_gram_tree_f64(h, pf, P(self.fm_part), T * self.nblk_r, self.nblk_r, 0,
                                 P(self.fm_sub)), "tree fm blocks")
 
