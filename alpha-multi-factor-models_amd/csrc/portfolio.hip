@@ -1752,16 +1752,51 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
         const u64 fm = __ballot(fits);
         const int c = fm == ~0ull ? 64 : __builtin_ctzll(~fm);   // prefix of dates that fits
         if (lane < c) offs[b][lane] = incl - len;
+        // the records' first 128 words for 16 dates at a time, every load issued before the LDS
+        // writes (round 4: a date-by-date copy waited one global-load latency per date, ~1 us,
+        // and the scan waited for it at the chunk barrier); longer records' tails after
+        constexpr int kB = 16;
+        for (int j0 = 0; j0 < c; j0 += kB) {
+            int v0[kB], v1[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int j = j0 + u < c ? j0 + u : c - 1;
+                const int l = __shfl(len, j, 64);
+                const int32_t* src = rec + (i0 + j) * kRec;
+                v0[u] = lane < l ? src[lane] : 0;
+                v1[u] = lane + 64 < l ? src[lane + 64] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int j = j0 + u < c ? j0 + u : c - 1;
+                const int o = __shfl(incl - len, j, 64), l = __shfl(len, j, 64);
+                if (j0 + u < c) {
+                    if (lane < l) buf[b][o + lane] = v0[u];
+                    if (lane + 64 < l) buf[b][o + lane + 64] = v1[u];
+                }
+            }
+        }
         for (int j = 0; j < c; ++j) {
             const int o = __shfl(incl - len, j, 64), l = __shfl(len, j, 64);
+            if (l <= 128) continue;                                  // (uniform)
             const int32_t* src = rec + (i0 + j) * kRec;
-            for (int e = lane; e < l; e += 64) buf[b][o + e] = src[e];
+            for (int e = 128 + lane; e < l; e += 64) buf[b][o + e] = src[e];
         }
-        for (int e = lane; e < (c + 1) * 4; e += 64) {
+        constexpr int kSumIt = ((kChunkDates + 1) * 4 + 63) / 64;   // all loads first
+        double sv[kSumIt];
+#pragma unroll
+        for (int u = 0; u < kSumIt; ++u) {
+            const int e = lane + 64 * u;
             const int64_t ii = i0 - 1 + e / 4;
-            const double v = ii >= 0 ? sums[(idx ? (int64_t)idx[ii] : ii) * 4 + e % 4] : 0.0;
-            sm[b][e / 4][e % 4] = v;
-            if (e % 4 >= 2) rcp[b][e / 4][e % 4 - 2] = 1.0 / v;
+            sv[u] = e < (c + 1) * 4 && ii >= 0 ? sums[(idx ? (int64_t)idx[ii] : ii) * 4 + e % 4] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kSumIt; ++u) {
+            const int e = lane + 64 * u;
+            if (e < (c + 1) * 4) {
+                sm[b][e / 4][e % 4] = sv[u];
+                if (e % 4 >= 2) rcp[b][e / 4][e % 4 - 2] = 1.0 / sv[u];
+            }
         }
         if (lane == 0) { cstart[b] = i0; ccount[b] = c; }
         return i0 + c;
