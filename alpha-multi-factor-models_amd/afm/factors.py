@@ -35,7 +35,7 @@ TARGET, TMR = COL["target"], COL["tmr_ret1d"]
 def factor_panel(grid: PanelGrid, out=None, nanfree=None, finite=None):
     """Run the factor kernel on a device-resident grid.
 
-    Returns ``(out, nanfree)``: ``out`` torch float64 ``[98][T][lda]`` (absent cells untouched,
+    Returns ``(out, nanfree)``: ``out`` torch float64 ``[98][T][lda]`` (absent cells NaN or untouched,
     NaN-initialised when allocated here), ``nanfree`` int64 ``[ceil(T/64)][lda]`` presence-and-
     no-NaN-in-96-factors bits (afm.h).  ``finite`` (optional, preallocated like ``nanfree``)
     receives the presence-and-all-96-finite bits."""

@@ -63,7 +63,8 @@ const char* afm_factor_name(int i);
 
 /* ---- I0-I16: factor panel -- replaces compute_factors(data) (No-talib.py:1-93) -----------
  * Inputs [T][lda]: close_price, volume, ret1d, excess_ret1d; valid_bits [ceil(T/64)][lda].
- * out: [AFM_N_FACTORS][T][lda]; cells of absent asset-days are left untouched.
+ * out: [AFM_N_FACTORS][T][lda]; cells of absent asset-days hold NaN in the date rows the kernel
+ * writes for their 64-asset block (a day with a present asset in the block), else untouched.
  * nanfree_bits [ceil(T/64)][lda]: present AND all 96 factor columns non-NaN (target/tmr_ret1d
  * excluded: their NaN-ness is read from their planes), i.e. the dropna() row mask of
  * No-talib.py:33 before the pass-through and label columns are considered.
