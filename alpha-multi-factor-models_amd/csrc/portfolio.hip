@@ -1583,30 +1583,38 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
     const int64_t si = idx ? idx[i] : i;             // book slots of this and the previous step
     const int64_t sp = i % seq == 0 ? -1 : (idx ? idx[i - 1] : i - 1);
     const bool active = sp >= 0 && k_out[sp] > 0;    // current_positions.dropna().empty -> 0
+    // both dates' books into LDS first (round 4: the membership tests below read them ~4k times
+    // per lane; from global memory each was a dependent load, ~0.2 ms per workgroup)
+    __shared__ int bk_cur[2 * kMaxK], bk_prev[2 * kMaxK];
+    int k = 0, kp = 0;
     if (active) {
-        const int k = k_out[si], kp = k_out[sp];
+        k = k_out[si];
+        kp = k_out[sp];
+        for (int e = tid; e < 2 * k; e += 64) bk_cur[e] = books[(si * 2 + e / k) * kMaxK + e % k];
+        for (int e = tid; e < 2 * kp; e += 64) bk_prev[e] = books[(sp * 2 + e / kp) * kMaxK + e % kp];
+    }
+    __syncthreads();
+    if (active) {
         for (int e = tid; e < 2 * kp; e += 64) {     // previous members predicted today
             const int side = e / kp, q = e % kp;
-            const int a = books[(sp * 2 + side) * kMaxK + q];
+            const int a = bk_prev[e];
             const int pz = upos[(((i - 1) * 2 + side) * 2 + 1) * kMaxK + q];
             if (pz < 0) continue;
             int ns = 2;
-            for (int s2 = 0; s2 < 2; ++s2)
-                for (int q2 = 0; q2 < k; ++q2)
-                    if (books[(si * 2 + s2) * kMaxK + q2] == a) ns = s2;
+            for (int q2 = 0; q2 < 2 * k; ++q2)
+                if (bk_cur[q2] == a) ns = q2 / k;
             const int slot = atomicAdd(&cnt, 1);
             pos_s[slot] = pz;
             code_s[slot] = side * 3 + ns;
         }
         for (int e = tid; e < 2 * k; e += 64) {      // today's members predicted yesterday only
             const int side = e / k, q = e % k;
-            const int a = books[(si * 2 + side) * kMaxK + q];
+            const int a = bk_cur[e];
             const int pz = upos[((i * 2 + side) * 2 + 0) * kMaxK + q];
             if (pz < 0) continue;
             bool inprev = false;
-            for (int s2 = 0; s2 < 2; ++s2)
-                for (int q2 = 0; q2 < kp; ++q2)
-                    if (books[(sp * 2 + s2) * kMaxK + q2] == a) inprev = true;
+            for (int q2 = 0; q2 < 2 * kp; ++q2)
+                if (bk_prev[q2] == a) inprev = true;
             if (inprev) continue;
             const int slot = atomicAdd(&cnt, 1);
             pos_s[slot] = pz;

@@ -178,6 +178,8 @@ def main():
     ap.add_argument("--top-n", type=int, default=10)
     ap.add_argument("--fm-free-cus", type=int, default=None,
                     help="PipelineConfig.fm_free_cus (CUs the FM side stream leaves free)")
+    ap.add_argument("--fm-fork", default=None,
+                    help="PipelineConfig.fm_fork (where the FM Grams fork off the main stream)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="time what ONE rank of an N-GPU job computes, on one GPU (collectives "
                          "replaced by local copies, afm.sharded.EmulatedComm): a per-rank proxy, "
@@ -214,9 +216,12 @@ def main():
     grid = afm.PanelGrid.from_panel(p, device=dev)
     del p
     n_ad = grid.n_asset_days()                         # the whole panel (strong scaling)
-    cfg = PipelineConfig(top_n=args.top_n)
+    place = {}
     if args.fm_free_cus is not None:
-        cfg = PipelineConfig(top_n=args.top_n, fm_free_cus=args.fm_free_cus)
+        place["fm_free_cus"] = args.fm_free_cus
+    if args.fm_fork is not None:
+        place["fm_fork"] = args.fm_fork
+    cfg = PipelineConfig(top_n=args.top_n, **place)
     if world > 1:
         from afm.sharded import EXCHANGE_STAGES, Comm, ShardedPipeline
         pipe = ShardedPipeline(grid, Comm(), cfg)

@@ -14,3 +14,7 @@ timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no
 python3 -c "import json; d=json.load(open('$o/bench.json')); print(d['ms_per_step'], d['stage_ms'], d['roofline']['frac'], d['roofline_next']['frac'])"
 timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --emulate-world 8 > $o/emu8.json 2> $o/emu8.err || { tail -5 $o/emu8.err; exit 1; }
 cat $o/emu8.json
+for f in rebalance gram; do
+  timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-variants --fm-fork $f > $o/bench_fork_$f.json 2> $o/bench_fork_$f.err || { tail -5 $o/bench_fork_$f.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$o/bench_fork_$f.json')); print('fm_fork $f', d['ms_per_step'], d['stage_ms'])"
+done
