@@ -1127,7 +1127,7 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
     LDS Smem& sm = *smp;
     const int64_t asset = block * kLanes + lane_asset(lane);
     const int c0 = a.c0, nch = a.c1;
-    double pc[kChunk], pv[kChunk];
+    double pcA[kChunk], pvA[kChunk], pcB[kChunk], pvB[kChunk];   // two chunks of loads in flight
     u64 vb = a.vbits[(int64_t)((c0 * kChunk) >> 6) * a.lda + asset];
     int pmod = 0;                                   // observations before the staged chunk, mod kRing
     int run = 0;                                    // consecutive in-range observations (cap kClean)
@@ -1141,7 +1141,10 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         run = (int)st[(2 * kRing + 1) * kLanes + lane];
         cnt = (int)st[(2 * kRing + 2) * kLanes + lane];
     }
-    auto load = [&](int ch) {
+    u64 vbn = 0ull;                                 // the next presence word, loaded early
+    auto load = [&](int ch, double (&pc)[kChunk], double (&pv)[kChunk]) {
+        if (((ch * kChunk) & 63) == 0 && ch > c0)
+            vbn = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
             const int64_t t = (int64_t)ch * kChunk + j;
@@ -1150,9 +1153,10 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
             pv[j] = in ? a.volume[t * a.lda + asset] : 0.0;
         }
     };
-    auto stage = [&](int ch) {                      // registers (chunk ch) -> ring + cbyte
+    // registers (chunk ch) -> ring + cbyte
+    auto stage = [&](int ch, const double (&pc)[kChunk], const double (&pv)[kChunk]) {
         const int sh = (ch * kChunk) & 63;
-        if (sh == 0 && ch > c0) vb = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
+        if (sh == 0 && ch > c0) vb = vbn;
         const u64 cb = (vb >> sh) & ((1ull << kChunk) - 1ull);
         int q = pmod;
         bool ok = true, warm = true;
@@ -1173,19 +1177,28 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         sm.cbyte[ch % kNCh][lane] = (int)cb;
         sm.okbyte[ch % kNCh][lane] = !a.fast ? 0 : ok ? 2 : warm ? 1 : 0;
     };
-    for (int ch = c0; ch < nch; ++ch) {
-        if (ch == c0) load(ch);
-        if (ch - kNCh >= c0) {                      // every job wave done with chunk ch - kNCh
-            const int need = ch - kNCh + 1;
-            while (__builtin_amdgcn_ballot_w64(lane < njobs && sm.done[lane < njobs ? lane : 0] < need)
-                   != 0ull) {
-                asm volatile("" ::: "memory");
-                __builtin_amdgcn_s_sleep(1);
-            }
+    auto wait_jobs = [&](int ch) {                  // every job wave done with chunk ch - kNCh
+        if (ch - kNCh < c0) return;
+        const int need = ch - kNCh + 1;
+        while (__builtin_amdgcn_ballot_w64(lane < njobs && sm.done[lane < njobs ? lane : 0] < need)
+               != 0ull) {
+            asm volatile("" ::: "memory");
+            __builtin_amdgcn_s_sleep(1);
         }
-        stage(ch);
+    };
+    // chunk ch is staged from registers loaded two chunks earlier (8 days of load latency covered)
+    load(c0, pcA, pvA);
+    if (c0 + 1 < nch) load(c0 + 1, pcB, pvB);
+    for (int ch = c0; ch < nch; ch += 2) {
+        wait_jobs(ch);
+        stage(ch, pcA, pvA);
         lds_publish(&sm.staged, ch + 1, lane);
-        if (ch + 1 < nch) load(ch + 1);
+        if (ch + 2 < nch) load(ch + 2, pcA, pvA);
+        if (ch + 1 >= nch) break;
+        wait_jobs(ch + 1);
+        stage(ch + 1, pcB, pvB);
+        lds_publish(&sm.staged, ch + 2, lane);
+        if (ch + 3 < nch) load(ch + 3, pcB, pvB);
     }
     if (st) {                                       // for the next slab (the ring's final
         for (int q = 0; q < kRing; ++q) {           // contents: the job waves only read it)

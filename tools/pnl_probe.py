@@ -1,0 +1,50 @@
+"""Time the PnL recursion (afm_pnl_scan_f64: turnover_terms_kernel + pnl_scan_kernel) alone on the
+bench workload's rebalance outputs (after one pipeline step), and the turnover kernel's records.
+
+    python tools/pnl_probe.py [--assets 10000 --days 5040 --reps 10]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "alpha-multi-factor-models_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--assets", type=int, default=10000)
+    ap.add_argument("--days", type=int, default=5040)
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import afm
+    from afm import _lib
+    from afm.pipeline import Pipeline, PipelineConfig
+    from afm.synthetic import make_panel
+    grid = afm.PanelGrid.from_panel(make_panel(a.assets, a.days, seed=2023, tradable_p=0.9))
+    pipe = Pipeline(grid, PipelineConfig())
+    pipe.step()
+    torch.cuda.synchronize()
+    L, P = _lib.lib(), _lib.ptr
+    r, q, c = pipe.reb, pipe.pnl, pipe.cfg
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for _ in range(a.reps):
+        h = _lib.Context.get().bind_stream()
+        ev[0].record()
+        _lib.check(L.afm_pnl_scan_f64(h, pipe.nd, P(r["k"]), P(r["books"]), P(r["sums"]),
+                                      P(r["upos"]), P(r["usize"]), c.v0, c.rate, P(q["value"]),
+                                      P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])), "pnl")
+        ev[1].record()
+        torch.cuda.synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]))
+    us = pipe.reb["usize"].cpu().numpy()
+    print(f"A={a.assets} dates={pipe.nd}: afm_pnl_scan_f64 alone {np.median(ts):.3f} ms "
+          f"(min {min(ts):.3f}) = {np.median(ts) * 1e3 / pipe.nd:.2f} us per date; union size "
+          f"median {int(np.median(us[:, 0]))}, max {int(us[:, 0].max())}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
