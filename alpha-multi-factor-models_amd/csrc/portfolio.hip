@@ -1830,7 +1830,7 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
             // date j's V-independent inputs, read one date ahead
             struct Pre {
                 const int* R;
-                int m, nint, L, code, en0, w0;
+                int m, nint, L, code, en0, w0, wd;
                 double s0, s1, s2, s3, r2, r3;
             };
             auto prefetch = [&](int j) {
@@ -1847,6 +1847,8 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                 const int* lend = f.R + 4 + (f.m > 0 ? f.m : 0) + f.nint;
                 f.en0 = f.m > 0 && f.L > 0 ? lend[0] : 0;
                 f.w0 = lane < f.en0 ? f.R[4 + f.m + lane] : 0;
+                // the dataflow evaluation's descriptor (internal node `lane`, level order)
+                f.wd = f.m > 0 && lane < f.nint ? f.R[4 + f.m + lane] : 0;
                 return f;
             };
             Pre cur = prefetch(0);
@@ -1871,25 +1873,41 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                     };
                     if (lane < m) node[lane] = leaf(f.code);
                     for (int e = lane + 64; e < m; e += 64) node[e] = leaf(R[4 + e]);
-                    const int* adds = R + 4 + m;
-                    const int* lend = adds + nint;
-                    // one DAG level per step, no lgkmcnt(0) wait (see above); the next level's
-                    // first add descriptor is fetched while this level's node reads are in flight
-                    int st = 0;
-                    int en = f.en0;
-                    int wcur = f.w0;
-                    for (int l = 0; l < L; ++l) {
-                        const int en2 = l + 1 < L ? lend[l + 1] : en;
-                        const int wnext = en + lane < en2 ? adds[en + lane] : 0;
-                        for (int e = st + lane; e < en; e += 64) {
-                            const int w = e == st + lane ? wcur : adds[e];
-                            node[m + e] = node[w & 0xffff] + node[w >> 16];
+                    if (nint <= 64 && nint > 0) {
+                        // dataflow: lane q recomputes internal node q from the current node
+                        // values L times (a node of level h is final after h passes); the
+                        // descriptors were read a date ahead, the root stays in its lane's register
+                        const int a0 = f.wd & 0xffff, b0 = f.wd >> 16;
+                        double v = 0.0;
+                        for (int l = 0; l < L; ++l) {
+                            v = node[a0] + node[b0];
+                            if (lane < nint) node[m + lane] = v;
                         }
-                        st = en;
-                        en = en2;
-                        wcur = wnext;
+                        const uint64_t rb = __builtin_bit_cast(uint64_t, v);
+                        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)rb, nint - 1);
+                        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(rb >> 32), nint - 1);
+                        to = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo) / 2;
+                    } else {                          // the level-by-level path
+                        const int* adds = R + 4 + m;
+                        const int* lend = adds + nint;
+                        // one DAG level per step, no lgkmcnt(0) wait (see above); the next level's
+                        // first add descriptor is fetched while this level's node reads are in flight
+                        int st = 0;
+                        int en = f.en0;
+                        int wcur = f.w0;
+                        for (int l = 0; l < L; ++l) {
+                            const int en2 = l + 1 < L ? lend[l + 1] : en;
+                            const int wnext = en + lane < en2 ? adds[en + lane] : 0;
+                            for (int e = st + lane; e < en; e += 64) {
+                                const int w = e == st + lane ? wcur : adds[e];
+                                node[m + e] = node[w & 0xffff] + node[w >> 16];
+                            }
+                            st = en;
+                            en = en2;
+                            wcur = wnext;
+                        }
+                        to = node[nint > 0 ? m + nint - 1 : 0] / 2;
                     }
-                    to = node[nint > 0 ? m + nint - 1 : 0] / 2;
                 }
                 double daily = (f.s0 - f.s1) / 2;
                 daily -= mdiv(to * rate, V, rv);
