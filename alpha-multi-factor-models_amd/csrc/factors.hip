@@ -23,11 +23,12 @@
 //    prefetches and streams stores must drain its stores before it can use a prefetched value).
 //  * Windows are positional over each asset's PRESENT days (holes and listing gaps do not count,
 //    No-talib.py:5-6); the ring is indexed by the lane's observation count (mod kRing).
-//  * Time advances in chunks of kChunk = 4 calendar days, handed from the loader to the job waves
-//    through LDS counters (no workgroup barrier after the first; see kNCh): the job waves step
-//    their jobs over a chunk's present days and stream their output columns (16-B stores of two
-//    columns, see lane_asset) while the loader stages the next chunks.  Cells of absent
-//    asset-days in a date row the wave writes hold NaN.
+//  * Time advances in chunks of kChunk = 8 calendar days, one barrier per chunk: the job waves
+//    step their jobs over chunk c's present days and stream their output columns (16-B stores of
+//    two columns, see lane_asset) while the loader writes chunk c+1 into the ring and issues the
+//    loads of chunk c+2.  Cells of absent asset-days in a date row the wave writes hold NaN.
+//    (Round 4 measured a barrier-free hand-off -- LDS counters, 4- or 8-day chunks, up to 3
+//    chunks of skew between job waves: 11.6-11.9 vs 10.6-10.8 ms at config C)
 //  * Divisions by an observation count (window means, Welford updates, variances, PSY) use a
 //    correctly rounded reciprocal table and one Markstein correction -- the exactly rounded
 //    quotient for every integer divisor <= 64 (FMA; no contraction elsewhere); ewm skips its
@@ -47,18 +48,10 @@ namespace afm {
 namespace {
 
 constexpr int kLanes = 64;
-constexpr int kChunk = 4;
-// Round 4: no workgroup barrier per chunk.  The loader publishes each staged chunk through an LDS
-// counter and each job wave its completed chunks through its own; the loader may stage chunk c
-// once every job wave of its item has completed chunk c - kNCh, so the fastest job wave can run up
-// to kNCh - 1 chunks (12 days) ahead of the slowest.  (With one barrier per 8-day chunk every
-// wave waited for the item pair's slowest wave on every chunk -- ~27 % of each wave's cycles at
-// config C, r4_c_wave_profile.txt -- although no wave's own work was that uneven: the stalls of
-// the output stream land on different waves on different days.)  The ring holds the scan's
-// lookback (57 observations) plus kNCh chunks: the loader's writes of chunk c replace
-// observations that only chunks <= c - kNCh still read.
-constexpr int kNCh = 4;
-constexpr int kRing = 57 + 1 + kNCh * kChunk;
+constexpr int kChunk = 8;
+// the loader fills chunk c+1 while the job waves scan chunk c: the ring must hold the scan's
+// lookback (57) plus two chunks
+constexpr int kRing = 57 + 2 * kChunk + 1;
 // job waves per 64-asset block (the partition W0..W14 below): three items of 5 job waves + a
 // loader, two items per workgroup = 3 waves per SIMD at <= 168 VGPRs.  (A 21-set partition at
 // 4 waves per SIMD / 128 VGPRs measured no faster: DESIGN.md §4, round 3.)
@@ -88,26 +81,9 @@ struct Smem {
     double c[kRing][kLanes];   // close ring (by observation index mod kRing)
     double v[kRing][kLanes];   // volume ring
     double rtab[128];          // rtab[n] = 1.0 / n (IEEE), rtab[0] = +inf; indexed n & 127
-    int cbyte[kNCh][kLanes];   // presence bits of chunk c (slot c % kNCh), written by the loader
-    int okbyte[kNCh][kLanes];  // chunk c: 2 every present day clean (kClean), 1 warm, 0 general
-    int staged;                // chunks staged: every chunk < staged is in the ring (absolute)
-    int done[16];              // per job wave: every chunk < done[w] completed (absolute)
+    int cbyte[2][kLanes];      // presence bits of chunk c (parity c & 1), written by the loader
+    int okbyte[2][kLanes];     // chunk c: 2 every present day clean (kClean), 1 warm, 0 general
 };
-
-// LDS hand-offs inside one item (no workgroup barrier): a plain LDS read of a counter (ds_read --
-// an atomic or a fence would wait on the job waves' outstanding output stores too), and a
-// publish after the wave's own LDS accesses have completed.  One wave's LDS operations execute in
-// order, so a ring read issued after the counter read sees the loader's earlier ring writes.
-__device__ __forceinline__ int lds_peek(const LDS int* p) {
-    const int v = *(const volatile LDS int*)p;
-    asm volatile("" ::: "memory");
-    return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ void lds_publish(LDS int* p, int v, int lane) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) *(volatile LDS int*)p = v;
-    asm volatile("" ::: "memory");
-}
 
 // ---- clean windows ----------------------------------------------------------------------------
 // A present day is CLEAN when it and the kClean - 1 observations before it all have close and
@@ -1119,15 +1095,15 @@ using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>, Ema<6>>;
 #define AFM_FP_FOR_SETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
     X(13) X(14)
 
-// The loader wave: global -> ring, chunk by chunk as the job waves release ring rows (kNCh), the
-// next chunk's loads in flight while it waits.  It also publishes, per lane and chunk, whether
-// every present day of the chunk is clean (kClean).
+// The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
+// job waves (one per chunk).  It also publishes, per lane and
+// chunk, whether every present day of the chunk is clean (kClean).
 __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane, int64_t block,
-                                          GLB double* st, int njobs) {
+                                          GLB double* st) {
     LDS Smem& sm = *smp;
     const int64_t asset = block * kLanes + lane_asset(lane);
     const int c0 = a.c0, nch = a.c1;
-    double pcA[kChunk], pvA[kChunk], pcB[kChunk], pvB[kChunk];   // two chunks of loads in flight
+    double pc[kChunk], pv[kChunk];
     u64 vb = a.vbits[(int64_t)((c0 * kChunk) >> 6) * a.lda + asset];
     int pmod = 0;                                   // observations before the staged chunk, mod kRing
     int run = 0;                                    // consecutive in-range observations (cap kClean)
@@ -1141,10 +1117,7 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         run = (int)st[(2 * kRing + 1) * kLanes + lane];
         cnt = (int)st[(2 * kRing + 2) * kLanes + lane];
     }
-    u64 vbn = 0ull;                                 // the next presence word, loaded early
-    auto load = [&](int ch, double (&pc)[kChunk], double (&pv)[kChunk]) {
-        if (((ch * kChunk) & 63) == 0 && ch > c0)
-            vbn = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
+    auto load = [&](int ch) {
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
             const int64_t t = (int64_t)ch * kChunk + j;
@@ -1153,11 +1126,10 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
             pv[j] = in ? a.volume[t * a.lda + asset] : 0.0;
         }
     };
-    // registers (chunk ch) -> ring + cbyte
-    auto stage = [&](int ch, const double (&pc)[kChunk], const double (&pv)[kChunk]) {
+    auto stage = [&](int ch) {                      // registers (chunk ch) -> ring + cbyte
         const int sh = (ch * kChunk) & 63;
-        if (sh == 0 && ch > c0) vb = vbn;
-        const u64 cb = (vb >> sh) & ((1ull << kChunk) - 1ull);
+        if (sh == 0 && ch > c0) vb = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
+        const u64 cb = (vb >> sh) & 0xffull;
         int q = pmod;
         bool ok = true, warm = true;
 #pragma unroll
@@ -1174,34 +1146,22 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
             }
         }
         pmod = q;
-        sm.cbyte[ch % kNCh][lane] = (int)cb;
-        sm.okbyte[ch % kNCh][lane] = !a.fast ? 0 : ok ? 2 : warm ? 1 : 0;
+        sm.cbyte[ch & 1][lane] = (int)cb;
+        sm.okbyte[ch & 1][lane] = !a.fast ? 0 : ok ? 2 : warm ? 1 : 0;
     };
-    auto wait_jobs = [&](int ch) {                  // every job wave done with chunk ch - kNCh
-        if (ch - kNCh < c0) return;
-        const int need = ch - kNCh + 1;
-        while (__builtin_amdgcn_ballot_w64(lane < njobs && sm.done[lane < njobs ? lane : 0] < need)
-               != 0ull) {
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_s_sleep(1);
+    load(c0);
+    stage(c0);
+    if (c0 + 1 < nch) load(c0 + 1);
+    lds_barrier();                                  // chunk c0 staged
+    for (int ch = c0; ch < nch; ++ch) {
+        if (ch + 1 < nch) {
+            stage(ch + 1);
+            if (ch + 2 < nch) load(ch + 2);
         }
-    };
-    // chunk ch is staged from registers loaded two chunks earlier (8 days of load latency covered)
-    load(c0, pcA, pvA);
-    if (c0 + 1 < nch) load(c0 + 1, pcB, pvB);
-    for (int ch = c0; ch < nch; ch += 2) {
-        wait_jobs(ch);
-        stage(ch, pcA, pvA);
-        lds_publish(&sm.staged, ch + 1, lane);
-        if (ch + 2 < nch) load(ch + 2, pcA, pvA);
-        if (ch + 1 >= nch) break;
-        wait_jobs(ch + 1);
-        stage(ch + 1, pcB, pvB);
-        lds_publish(&sm.staged, ch + 2, lane);
-        if (ch + 3 < nch) load(ch + 3, pcB, pvB);
+        lds_barrier();
     }
-    if (st) {                                       // for the next slab (the ring's final
-        for (int q = 0; q < kRing; ++q) {           // contents: the job waves only read it)
+    if (st) {                                       // for the next slab (after the last barrier:
+        for (int q = 0; q < kRing; ++q) {           // no job wave reads the ring any more)
             st[(2 * q) * kLanes + lane] = sm.c[q][lane];
             st[(2 * q + 1) * kLanes + lane] = sm.v[q][lane];
         }
@@ -1209,6 +1169,13 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         st[(2 * kRing + 1) * kLanes + lane] = (double)run;
         st[(2 * kRing + 2) * kLanes + lane] = (double)cnt;
     }
+}
+
+// A wave with no item (odd item count in the paired launch): the loader's barrier sequence.
+__device__ __forceinline__ void idle_wave(const Args& a) {
+    const int nch = a.c1;
+    lds_barrier();
+    for (int ch = a.c0; ch < nch; ++ch) lds_barrier();
 }
 
 // A job wave's complete state between two time slabs (stored lane-interleaved, 8-B words)
@@ -1260,6 +1227,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
         pmod = js.pmod;
     }
     u64 nb = 0ull, fb = 0ull;   // this wave's NaN / non-finite bits of the current 64-day word
+    lds_barrier();              // chunk 0 staged
 #ifdef AFM_FP_PROFILE
     const long long tstart = __builtin_readcyclecounter();
     const long long treal = (long long)__builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
@@ -1425,18 +1393,17 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
             nb = 0ull;
             fb = 0ull;
         }
-        lds_publish(&sm.done[wave], ch + 1, lane);          // its ring rows are free
-    };
-    int ch = c0;
-    auto is_clean = [&](int c) {                            // after the loader has staged c
 #ifdef AFM_FP_PROFILE
         const long long tb = __builtin_readcyclecounter();
-#endif
-        while (lds_peek(&sm.staged) <= c) __builtin_amdgcn_s_sleep(1);
-#ifdef AFM_FP_PROFILE
+        lds_barrier();
         twait += __builtin_readcyclecounter() - tb;
+#else
+        lds_barrier();
 #endif
-        return __builtin_amdgcn_ballot_w64(sm.okbyte[c % kNCh][lane] != 2) == 0ull;
+    };
+    int ch = c0;
+    auto is_clean = [&](int c) {
+        return __builtin_amdgcn_ballot_w64(sm.okbyte[c & 1][lane] != 2) == 0ull;
     };
     while (ch < nch) {
         if (is_clean(ch)) {
@@ -1447,22 +1414,22 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
             // stores too, so that wait would drain them on every step
             {
                 unsigned n8 = 0u, f8 = 0u;
-                fast_chunk(ch, (unsigned)sm.cbyte[ch % kNCh][lane], n8, f8);
+                fast_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], n8, f8);
                 chunk_end(ch, n8, f8);
                 ++ch;
             }
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
             while (ch < nch && is_clean(ch)) {              // the hot loop
                 unsigned n8 = 0u, f8 = 0u;
-                fast_chunk(ch, (unsigned)sm.cbyte[ch % kNCh][lane], n8, f8);
+                fast_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], n8, f8);
                 chunk_end(ch, n8, f8);
                 ++ch;
             }
         } else {                                            // one warm or general chunk
-            const int okl = sm.okbyte[ch % kNCh][lane];
+            const int okl = sm.okbyte[ch & 1][lane];
             const bool warm = __builtin_amdgcn_ballot_w64(okl == 0) == 0ull;
             unsigned n8 = 0u, f8 = 0u;
-            slow_chunk(ch, (unsigned)sm.cbyte[ch % kNCh][lane], warm, n8, f8);
+            slow_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], warm, n8, f8);
             chunk_end(ch, n8, f8);
             ++ch;
         }
@@ -1534,17 +1501,11 @@ void factor_panel_kernel(Args a) {
     const int half = PAIR ? (wall >= J + 1 ? 1 : 0) : 0;
     const int pos = wall - half * (J + 1);
     LDS Smem* sm = (LDS Smem*)sm_dyn + half;
-    // the reciprocal table and the item's hand-off counters; the workgroup's one barrier
-    const int ltid = (int)threadIdx.x - half * (J + 1) * kLanes;
-    if (ltid < 128) sm->rtab[ltid] = 1.0 / (double)ltid;
-    if (ltid == 0) sm->staged = a.c0;
-    if (ltid < 16) sm->done[ltid] = a.c0;
-    lds_barrier();
     int type;
     int64_t block;
     if (PAIR) {
         const int64_t item = 2 * (int64_t)blockIdx.x + half;
-        if (item >= (int64_t)a.nblk * TYPES) return;         // (odd item count: an idle half)
+        if (item >= (int64_t)a.nblk * TYPES) { idle_wave(a); return; }
         type = (int)(item / a.nblk);
         block = item % a.nblk;
     } else {
@@ -1553,10 +1514,13 @@ void factor_panel_kernel(Args a) {
     }
     // job index of this wave (J = the loader)
     const int wave = PAIR && TYPES == 3 ? (int)kPairLayout[type][half][pos] : pos;
+    const int ltid = (int)threadIdx.x - half * (J + 1) * kLanes;
+    if (ltid < 128) sm->rtab[ltid] = 1.0 / (double)ltid;
+    // (the loader's first barrier also publishes rtab)
     // this wave's slab-carry state slot
     GLB double* stp = a.state ? a.state + (((block * TYPES + type) * (J + 1) + wave) *
                                            (int64_t)kStateWords * kLanes) : nullptr;
-    if (wave == J) { load_wave(a, sm, lane, block, stp, J); return; }
+    if (wave == J) { load_wave(a, sm, lane, block, stp); return; }
     // this type's partial-mask planes (keeps the type out of the job waves' registers)
     Args at = a;
     const int64_t w0 = ((int64_t)a.c0 * kChunk) >> 6;
