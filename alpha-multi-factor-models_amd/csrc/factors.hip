@@ -1531,7 +1531,11 @@ void factor_panel_kernel(Args a) {
     at.pslot = (int)(block * TYPES + type);          // profile slot of this item
 #endif
     switch (type * J + wave) {
+#ifdef AFM_FP_ONLY   // instruction census (tools/pack_census.sh): one job set's code only
+#define AFM_FP_CASE(k) case k: if (k == AFM_FP_ONLY) run_wave<W##k>(at, sm, 0, wave, lane, block, stp); break;
+#else
 #define AFM_FP_CASE(k) case k: run_wave<W##k>(at, sm, 0, wave, lane, block, stp); break;
+#endif
         AFM_FP_FOR_SETS(AFM_FP_CASE)
 #undef AFM_FP_CASE
         default: break;
