@@ -1069,29 +1069,35 @@ struct Pack<H, R...> {
     }
 };
 
-// Static job partition over the 15 job waves of one workgroup (LPT on the per-job VALU count of
-// the compiled step: Corr ~550, RetSd5x15 ~360, VolSd5x15 ~290, BB ~220, VWMA ~170, RetSd3 /
-// VolSd3 / PvtObvPsy ~155, RSI ~115, SMA / MomAccelRocr ~100, MACD ~75, EMA ~60; ~620 per wave),
-// then waves placed so the four SIMDs (waves w, w+4, w+8, w+12; the loader shares SIMD 3) carry
-// equal totals.  Round 2: SMA_6 moved from W1 to W13 and EMA_6 from W8 to W14 so the three 3-way
-// item types take equal time (per-type max 25.0 / 25.0 / 22.2 -> 25.1 / 25.1 / 24.1 Mcycles,
-// 12.28 -> 11.46 ms at config C, no spill in the fast steps; a move that made the fast steps
-// spill measured 14.7 ms).
-using W0 = Pack<Bbands<14>, Vwma<30>, MomAccelRocr<32>, Sma<42>, Ema<50>>;
-using W1 = Pack<Bbands<44>, Vwma<50>, Sma<38>, Ema<46>>;
-using W2 = Pack<Bbands<50>, RetSd3, MomAccelRocr<26>, Sma<34>, Ema<42>>;
-using W3 = Pack<Bbands<56>, VolSd3, MomAccelRocr<20>, Sma<30>, Ema<38>>;
-using W4 = Pack<Vwma<6>, Vwma<18>, Rsi<8>, Sma<18>, Ema<18>>;
-using W5 = Pack<RetSd5x15, MomAccelRocr<14>, Sma<14>, Ema<14>>;
-using W6 = Pack<Bbands<38>, Vwma<46>, MomAccelRocr<56>, Macd<24>, Ema<34>>;
-using W7 = Pack<Bbands<32>, Vwma<42>, MomAccelRocr<50>, Macd<18>, Ema<30>>;
-using W8 = Pack<VolSd5x15, PvtObvPsy, Sma<10>>;
-using W9 = Pack<Corr<5, true>, Ema<10>>;
-using W10 = Pack<Vwma<14>, Vwma<26>, Rsi<20>, Sma<26>, Ema<26>>;
-using W11 = Pack<Vwma<10>, Vwma<22>, Rsi<14>, Sma<22>, Ema<22>>;
-using W12 = Pack<Corr<15, false>, Macd<30>>;
-using W13 = Pack<Bbands<20>, Vwma<34>, MomAccelRocr<38>, Sma<46>, Sma<6>>;
-using W14 = Pack<Bbands<26>, Vwma<38>, MomAccelRocr<44>, Sma<50>, Ema<6>>;
+// Static job partition over the 15 job waves of one block: 3 item types of 5 job sets.
+// Round 4: per type three light sets (the two rolling correlations alone, ...) at wave positions
+// 0, 2, 4 -- the SIMDs that carry three job waves of a paired workgroup -- and two heavy ones
+// (6-7 moving sums / bands) at positions 1, 3, the SIMDs the loaders share.  Config C: the same
+// time as the round-3 partition (10.3-10.7 ms, the kernel is bound by its write stream there);
+// at 1,250 assets, where each set runs alone on its SIMD (the 15-way split), 4.06 vs 4.30-4.54 ms
+// -- the correlations no longer share a wave (tools/gpu_r4i.sh, profiles/r4_i_partition_ab.txt).
+// A variant that moved one moving sum from each heavy set to a light one ran slower at both
+// sizes (11.0 / 4.7 ms).  The heavy sets' fast steps keep <= 8 scratch accesses (slab entry
+// reloads; the day loop's chains have none).
+#ifdef AFM_FP_CENSUS_W0     // instruction census of one job alone (tools/job_census.sh)
+using W0 = Pack<AFM_FP_CENSUS_W0>;
+#else
+using W0 = Pack<Corr<5, true>>;
+#endif
+using W1 = Pack<Bbands<32>, Vwma<30>, MomAccelRocr<32>, Ema<30>, Ema<6>, Sma<30>, Sma<18>>;
+using W2 = Pack<Bbands<14>, Vwma<14>, Ema<14>>;
+using W3 = Pack<Bbands<38>, Vwma<38>, MomAccelRocr<38>, Ema<38>, Ema<10>, Sma<38>, Sma<22>>;
+using W4 = Pack<Rsi<20>, Vwma<22>, MomAccelRocr<14>, Sma<14>, Macd<18>>;
+using W5 = Pack<Corr<15, false>>;
+using W6 = Pack<Bbands<44>, Vwma<42>, MomAccelRocr<44>, Ema<42>, Ema<22>, Sma<42>, Sma<26>>;
+using W7 = Pack<Bbands<20>, Vwma<18>, Ema<18>>;
+using W8 = Pack<Bbands<50>, Vwma<46>, MomAccelRocr<50>, Ema<46>, Ema<50>, Sma<46>, Sma<34>>;
+using W9 = Pack<RetSd5x15, VolSd3, Sma<6>>;
+using W10 = Pack<VolSd5x15, Rsi<8>>;
+using W11 = Pack<Bbands<56>, Vwma<50>, Vwma<34>, MomAccelRocr<56>, Sma<50>>;
+using W12 = Pack<PvtObvPsy, RetSd3, Rsi<14>, Sma<10>>;
+using W13 = Pack<Vwma<6>, Vwma<10>, MomAccelRocr<20>, MomAccelRocr<26>, Ema<34>, Macd<24>, Macd<30>>;
+using W14 = Pack<Bbands<26>, Vwma<26>, Ema<26>>;
 #define AFM_FP_FOR_SETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
     X(13) X(14)
 
@@ -1472,15 +1478,10 @@ constexpr int kStateWords = AFM_FP_FOR_SETS(AFM_FP_STATE_WORDS) 2 * kRing + 3
 // of 6 waves and 78 KB of LDS; at 168 VGPRs (3 waves / SIMD) two separate 6-wave workgroups
 // rarely co-reside on a CU (their waves land 2-2-1-1 on the SIMDs), so half of them ran in a
 // second round; paired, 236 workgroups of 12 waves (3 per SIMD, 156 KB LDS) are all resident.
-// Paired 3-way launch: job (0-4) or loader (5) run at wave position k of each half, per type.
-// Wave w of a workgroup issues on SIMD w % 4; the layouts minimise the busiest SIMD's measured
-// cycles (tools/wave_profile.py; type 1: 61.3 -> 55.0 Mcycles; round 2 re-checked for the new
-// partition with AFM_FP_LAYOUT, tools/gpu_layout.sh: four other layouts per type, none faster).
-__constant__ signed char kPairLayout[3][2][6] = {
-    {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
-    {{0, 2, 3, 4, 1, 5}, {1, 2, 3, 4, 0, 5}},
-    {{0, 2, 1, 4, 3, 5}, {0, 2, 1, 4, 3, 5}},
-};
+// Paired 3-way launch: job set k (0-4) or the loader (5) at wave position k of each half.  Wave
+// w of a workgroup issues on SIMD w % 4, so positions 0, 2, 4 of the two halves share SIMDs 0 and
+// 2 three to a SIMD, and positions 1, 3 share SIMDs 1 and 3 with the loaders (the partition above
+// puts the light sets at 0, 2, 4).
 // waves per SIMD a launch shape needs resident (the VGPR budget): the paired 3-way launch fills
 // the CU's four SIMDs evenly; the other splits allow 2 (256 VGPRs)
 template <int TYPES, bool PAIR>
@@ -1513,7 +1514,7 @@ void factor_panel_kernel(Args a) {
         block = blockIdx.x / TYPES;
     }
     // job index of this wave (J = the loader)
-    const int wave = PAIR && TYPES == 3 ? (int)kPairLayout[type][half][pos] : pos;
+    const int wave = pos;
     const int ltid = (int)threadIdx.x - half * (J + 1) * kLanes;
     if (ltid < 128) sm->rtab[ltid] = 1.0 / (double)ltid;
     // (the loader's first barrier also publishes rtab)
