@@ -107,73 +107,46 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
         const double tmp = q - h;
         return (positive && tmp < 0) ? 0.0 : (tmp < 0 ? -0.0 : 0.0);
     };
-    // the first coordinate >= lo that can move (p: none); coordinates [lo, that) store the signed
-    // zero they would compute (exactly sklearn's no-ops)
-    auto next_movable = [&](int lo) {
-        const uint64_t m0 = __ballot(has0 && j0 >= lo && movable(qd0, q0, h0, w0));
-        const uint64_t m1 = __ballot(has1 && j1 >= lo && movable(qd1, q1, h1, w1));
-        const int nx = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : p);
-        if (has0 && j0 >= lo && j0 < nx && qd0 != 0.0) w0 = zero_of(q0, h0);
-        if (has1 && j1 >= lo && j1 < nx && qd1 != 0.0) w1 = zero_of(q1, h1);
-        return __builtin_amdgcn_readfirstlane(nx);
-    };
     for (n_iter = 0; n_iter < max_iter; ++n_iter) {
         double w_max = 0.0, d_w_max = 0.0;
-        int ii = next_movable(0);
-        // coordinate ii's row of Q (lane j: Q[ii][j]) and its scalars
-        double r0 = 0.0, r1 = 0.0, qii = 0.0, w_ii = 0.0, h_ii = 0.0, q_ii = 0.0, rd_ii = 0.0;
-        auto load = [&](int c) {
-            const double* row = Q + c * p;
-            r0 = has0 ? row[j0] : 0.0;
-            r1 = has1 ? row[j1] : 0.0;
-            qii = pick(qd0, qd1, c);
-            w_ii = pick(w0, w1, c);
-            h_ii = pick(h0, h1, c);
-            q_ii = pick(q0, q1, c);
-            rd_ii = pick(rd0, rd1, c);
-        };
-        if (ii < p) load(ii);
-        while (ii < p) {
-            // round 4 (dense fits: ~475 -> ~60 ns per moving coordinate): the likely next
-            // coordinate c -- the first later one with a nonzero weight, movable whatever H does --
-            // is read while this one computes, and its H[c] after this coordinate's two axpys is
-            // formed on the scalar path from H[c] before them (the same two fmas as lane c's), so
-            // the next soft-threshold step does not wait for the vector axpys, the ballot or the
-            // row read.  The ballot of the truly movable coordinates confirms c (else the row and
-            // scalars of the coordinate it names are read then).
-            const uint64_t c0m = __ballot(has0 && j0 > ii && w0 != 0.0 && qd0 != 0.0);
-            const uint64_t c1m = __ballot(has1 && j1 > ii && w1 != 0.0 && qd1 != 0.0);
-            const int c = __builtin_amdgcn_readfirstlane(
-                c0m ? __builtin_ctzll(c0m) : (c1m ? 64 + __builtin_ctzll(c1m) : p));
-            double cr0 = 0.0, cr1 = 0.0, cqd = 0.0, cw = 0.0, chb = 0.0, cq = 0.0, crd = 0.0, qic = 0.0;
-            if (c < p) {
-                const double* rowc = Q + c * p;
-                cr0 = has0 ? rowc[j0] : 0.0;
-                cr1 = has1 ? rowc[j1] : 0.0;
-                cqd = pick(qd0, qd1, c);
-                cw = pick(w0, w1, c);            // lane c's weight: this coordinate leaves it
-                chb = pick(h0, h1, c);           // H[c] before this coordinate's axpys
-                cq = pick(q0, q1, c);
-                crd = pick(rd0, rd1, c);
-                qic = pick(r0, r1, c);           // Q[ii][c]
+        for (int ii = 0; ii < p; ++ii) {
+            {   // skip coordinates [ii, next) that cannot move (exactly sklearn's no-ops)
+                const uint64_t m0 = __ballot(has0 && j0 >= ii && movable(qd0, q0, h0, w0));
+                const uint64_t m1 = __ballot(has1 && j1 >= ii && movable(qd1, q1, h1, w1));
+                const int next = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : p);
+                if (next > ii) {
+                    if (has0 && j0 >= ii && j0 < next && qd0 != 0.0) w0 = zero_of(q0, h0);
+                    if (has1 && j1 >= ii && j1 < next && qd1 != 0.0) w1 = zero_of(q1, h1);
+                    ii = __builtin_amdgcn_readfirstlane(next);
+                    if (ii >= p) break;
+                }
             }
-            const double tc = __builtin_fma(-w_ii, qic, chb);
-            // coordinate ii.  H[ii] after the first axpy is lane ii's own fma (r = Q[ii][ii]
-            // there): computed on the scalar path, so the step does not wait for the axpy
+            // (the ballot above never stops at a coordinate with a zero diagonal: not movable)
+            const double* row = Q + ii * p;
+            const double r0 = has0 ? row[j0] : 0.0, r1 = has1 ? row[j1] : 0.0;
+            const double qii = pick(qd0, qd1, ii);
+            const double w_ii = pick(w0, w1, ii);
+            // H[ii] after the first axpy is lane ii's own fma (r = Q[ii][ii] there): computed on
+            // the scalar path directly, so the step does not wait for the row read or the axpy
+            const double h_ii = pick(h0, h1, ii);
             const double hh = w_ii != 0.0 ? __builtin_fma(-w_ii, qii, h_ii) : h_ii;
             // the axpys run unconditionally: with a zero weight fma(+-0, r, h) = h for the finite
             // Gram (a zero h may change the sign of its zero, which reaches no weight: h enters
             // only through q - h and further fmas)
             h0 = __builtin_fma(-w_ii, r0, h0);
             h1 = __builtin_fma(-w_ii, r1, h1);
-            const double tmp = q_ii - hh;
+            const double tmp = pick(q0, q1, ii) - hh;
             double wn;
             if (positive && tmp < 0) {
                 wn = 0.0;
             } else {
                 const double num = fsign(tmp) * __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0);
-                if (all_rd) wn = div_r(num, qii + beta, rd_ii);
-                else wn = rd_ii != 0.0 ? div_r(num, qii + beta, rd_ii) : num / (qii + beta);
+                if (all_rd) {
+                    wn = div_r(num, qii + beta, pick(rd0, rd1, ii));
+                } else {
+                    const double rdi = pick(rd0, rd1, ii);
+                    wn = rdi != 0.0 ? div_r(num, qii + beta, rdi) : num / (qii + beta);
+                }
             }
             w0 = lane == ii ? wn : w0;
             w1 = lane + 64 == ii ? wn : w1;
@@ -182,22 +155,6 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
             // NaN-free: fmax keeps the larger, as the comparisons did
             d_w_max = __builtin_fmax(__builtin_fabs(wn - w_ii), d_w_max);
             w_max = __builtin_fmax(__builtin_fabs(wn), w_max);
-            // H[c] after both axpys (lane c's two fmas; tc does not wait for wn)
-            const double hc = __builtin_fma(wn, qic, tc);
-            const int nx = next_movable(ii + 1);
-            if (nx == c && c < p) {              // (uniform) the prefetched coordinate
-                ii = c;
-                r0 = cr0;
-                r1 = cr1;
-                qii = cqd;
-                w_ii = cw;
-                h_ii = hc;
-                q_ii = cq;
-                rd_ii = crd;
-            } else {
-                ii = nx;
-                if (ii < p) load(ii);
-            }
         }
         if (w_max == 0.0 || d_w_max / w_max < d_w_tol || n_iter == max_iter - 1) {
             double q_dot_w = 0.0, wh = 0.0, w_norm2 = 0.0, asum = 0.0, dual = 0.0;
