@@ -34,6 +34,7 @@ SIGNATURES = {
     "afm_factors_f64": (I32, [P, I64, I64, I64, P, P, P, P, P, P, P, P]),
     "afm_factors_state_bytes": (I64, [P, I64]),
     "afm_factors_slab_f64": (I32, [P, I64, I64, I64, I64, I64, P, P, P, P, P, P, P, P, P]),
+    "afm_factors_range_f64": (I32, [P, I64, I64, I64, I64, I64, P, P, P, P, P, P, P, P, P]),
     "afm_xs_gram_f64": (I32, [P, P, I64, I64, I64, I64, P, I32, I32, P, I64, I64, P, P]),
     "afm_ols_solve_f64": (I32, [P, P, P, I32, I64, DBL, P, P, P]),
     "afm_pool_moments_f64": (I32, [P, P, P, I32, I64, P, P]),
@@ -41,6 +42,7 @@ SIGNATURES = {
     "afm_pool_segments_f64": (I32, [P, P, P, I32, I64, I64, P, P]),
     "afm_labels_f64": (I32, [P, I64, I64, I64, I64, P, P, P, P, P]),
     "afm_drop_last_obs_bits": (I32, [P, I64, I64, P, P, P]),
+    "afm_drop_last_obs_bits_range": (I32, [P, I64, I64, P, P, P, I64, I64]),
     "afm_predict_f64": (I32, [P, P, I64, I64, I64, I64, P, I32, P, I64, P, I32, P]),
     "afm_fama_macbeth_f64": (I32, [P, P, P, I64, I32, P, P]),
     "afm_ols_residual_f64": (I32, [P, P, I64, I32, I32, P, P, P]),

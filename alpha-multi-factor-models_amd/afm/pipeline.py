@@ -111,6 +111,12 @@ class PipelineConfig:
     # stream, afm_stream_create_cu_mask), so the latency-bound tail beside the FM MFMA Grams keeps
     # whole CUs; 0 = an ordinary stream
     fm_free_cus: int = 0
+    # early_zstats -- the factor panel in two time slabs (afm_factors_range_f64): the train
+    # window's z statistics run on a side stream while the second slab builds (a shard's factor
+    # kernel leaves most of the GPU free: one wave per job set).  Measured at the N = 8 shard
+    # (1,280 assets): 8.97 ms per step either way -- the second slab is the ~17 % of dates after
+    # the train window, and the z statistics beside it ran 1.69 instead of 1.03 ms -- so off
+    early_zstats: bool = False
 
 
 @dataclass
@@ -366,6 +372,15 @@ class Pipeline:
             self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
         self.labels_done = torch.cuda.Event()
+        # early z statistics: the first slab ends at the first 64-date boundary past the train
+        # window (the slab API's alignment)
+        self.ta = min(((sp.tr1 + 63) // 64) * 64, T)
+        self.early = bool(c.early_zstats) and self.A_r > 0 and self.ta < T
+        if self.early:
+            nb = int(L.afm_factors_state_bytes(self.ctx.handle, self.A_r))
+            self.fstate = torch.empty(nb // 8 + 1, **f64)
+            self.slab1_done = torch.cuda.Event()
+            self.zstats_done = torch.cuda.Event()
 
     def n_asset_days_local(self) -> int:
         return int(self.g.valid.sum().item())
@@ -428,6 +443,56 @@ class Pipeline:
                                     P(self.fm_beta_own), P(self.fm_nobs_own),
                                     P(self.fm_rank_own)), "fm solve")
 
+    def _factors_early(self, h, lab_side, mark):
+        """The factor panel in two slabs [0, ta) and [ta, T) on the main stream; the train
+        window's z statistics (and the z-score row bits of the first slab) on the side stream
+        beside the second slab.  Bitwise the same panel, statistics and row sets as one call."""
+        import torch
+        L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+        g, sp, T, lda_r, p, ta = self.g, self.sp, self.T, self.lda_r, self.p, self.ta
+        A_r, wa = self.A_r, self.ta // 64
+        lab = (None, None) if lab_side else (P(g.ret1d), P(g.excess))
+        chk(L.afm_factors_range_f64(h, T, A_r, lda_r, 0, ta, P(g.close), P(g.volume), *lab,
+                                    P(g.vbits), P(self.out), P(self.nanfree), P(self.finite),
+                                    P(self.fstate)), "factors slab 1")
+        if lab_side:
+            with torch.cuda.stream(self.side2):
+                h2 = self.ctx.bind_stream()
+                chk(L.afm_labels_f64(h2, T, lda_r, 0, T, P(g.excess), P(g.ret1d), P(g.vbits),
+                                     P(self.out[TARGET]), P(self.out[TMR])), "labels")
+                self.labels_done.record(self.side2)
+            h = self.ctx.bind_stream()
+        for src, dst in ((self.nanfree, self.alldf), (self.finite, self.frows)):
+            chk(L.afm_drop_last_obs_bits_range(h, T, lda_r, P(g.vbits), P(src), P(dst), 0, ta),
+                "last-obs rows 1")
+        self.slab1_done.record(self.main)
+        with torch.cuda.stream(self.side):
+            hs = self.ctx.bind_stream()
+            self.side.wait_event(self.slab1_done)
+            if lab_side:
+                self.side.wait_event(self.labels_done)          # tmr_ret1d is a feature
+            mark("zstats", 0)
+            chk(L.afm_zscore_stats_f64(hs, P(self.out), T * lda_r, T, lda_r, P(self.feat), p,
+                                       P(self.alldf), 0, sp.tr1, P(self.mu), P(self.sd)),
+                "zscore stats")
+            chk(L.afm_zstats_finalize_f64(hs, P(self.mu), P(self.sd), p, lda_r, P(self.zs),
+                                          P(self.asset_ok)), "zstats finalize")
+            chk(L.afm_row_bits(hs, wa, lda_r, P(self.frows), None, P(self.asset_ok), 0, ta,
+                               P(self.zrows)), "z rows 1")
+            mark("zstats", 1)
+            self.zstats_done.record(self.side)
+        h = self.ctx.bind_stream()
+        chk(L.afm_factors_range_f64(h, T, A_r, lda_r, ta, T, P(g.close), P(g.volume), *lab,
+                                    P(g.vbits), P(self.out), P(self.nanfree), P(self.finite),
+                                    P(self.fstate)), "factors slab 2")
+        for src, dst in ((self.nanfree, self.alldf), (self.finite, self.frows)):
+            chk(L.afm_drop_last_obs_bits_range(h, T, lda_r, P(g.vbits), P(src), P(dst), ta, T),
+                "last-obs rows 2")
+        mark("factors", 1)
+        self.main.wait_event(self.zstats_done)
+        chk(L.afm_row_bits(h, self.nch - wa, lda_r, P(self.frows[wa:]), None, P(self.asset_ok),
+                           0, T - ta, P(self.zrows[wa:])), "z rows 2")
+
     def step(self, events: dict | None = None):
         """One pass of the chain.  ``events``: optional {stage: (start, end)} CUDA events."""
         import torch
@@ -449,7 +514,10 @@ class Pipeline:
             # one GPU: the two label planes on the side stream, enqueued after the factor kernel
             # (it runs on the CUs the factor workgroups leave free); zstats waits for them
             lab_side = W == 1 and c.labels_side
-            if self.A_r > 0:
+            if self.early:
+                self._factors_early(h, lab_side, mark)
+                h = self.ctx.bind_stream()
+            elif self.A_r > 0:
                 chk(L.afm_factors_f64(h, T, self.A_r, lda_r, P(g.close), P(g.volume),
                                       None if lab_side else P(g.ret1d),
                                       None if lab_side else P(g.excess), P(g.vbits), P(self.out),
@@ -466,9 +534,10 @@ class Pipeline:
                                              P(self.alldf)), "all_df rows")
                 chk(L.afm_drop_last_obs_bits(h, T, lda_r, P(g.vbits), P(self.finite),
                                              P(self.frows)), "finite rows")
-            mark("factors", 1)
-            mark("zstats", 0)
-            if self.A_r > 0:
+            if not self.early:
+                mark("factors", 1)
+                mark("zstats", 0)
+            if self.A_r > 0 and not self.early:
                 if lab_side:
                     self.main.wait_event(self.labels_done)          # tmr_ret1d is a feature
                 chk(L.afm_zscore_stats_f64(h, P(self.out), T * lda_r, T, lda_r, P(self.feat), p,

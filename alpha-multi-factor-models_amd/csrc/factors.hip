@@ -1619,9 +1619,11 @@ __global__ __launch_bounds__(256) void labels_kernel(int64_t T, int64_t t_begin,
 
 // out = in without each asset's last present day: the rows whose shift(-1) labels (target,
 // tmr_ret1d, No-talib.py:90-91) are NaN.  One thread per asset; words copied coalesced.
+// words [c0, c1) of out; the last observation from all nwords words of vbits
 __global__ __launch_bounds__(256) void drop_last_obs_kernel(int64_t nwords, int64_t lda,
                                                             const uint64_t* vbits,
-                                                            const uint64_t* in, uint64_t* out) {
+                                                            const uint64_t* in, uint64_t* out,
+                                                            int64_t c0, int64_t c1) {
     const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (a >= lda) return;
     int64_t last = -1;
@@ -1629,7 +1631,7 @@ __global__ __launch_bounds__(256) void drop_last_obs_kernel(int64_t nwords, int6
         const u64 w = vbits[c * lda + a];
         if (w) last = c * 64 + 63 - __builtin_clzll(w);
     }
-    for (int64_t c = 0; c < nwords; ++c) {
+    for (int64_t c = c0; c < c1; ++c) {
         u64 w = in[c * lda + a];
         if (last >= 0 && (last >> 6) == c) w &= ~(1ull << (last & 63));
         out[c * lda + a] = w;
@@ -1691,8 +1693,15 @@ static int launch_split(afm_ctx* ctx, int64_t nblk, const afm::Args& a) {
 static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0, int64_t t1,
                         const double* close, const double* volume, const double* ret1d,
                         const double* excess, const uint64_t* valid_bits, double* out,
-                        uint64_t* nanfree_bits, uint64_t* finite_bits, double* state) {
+                        uint64_t* nanfree_bits, uint64_t* finite_bits, double* state,
+                        bool full = false) {
+    // full: out / nanfree / finite are the whole [T]-date panel and bit words (the slab's rows
+    // and words written in place); else they hold the slab's dates only
     const int64_t nwords = (t1 - t0 + 63) / 64;                   // the slab's mask words
+    if (full) {
+        nanfree_bits += (t0 / 64) * lda;
+        if (finite_bits) finite_bits += (t0 / 64) * lda;
+    }
     const int64_t nblk = (A + 63) / 64;
     const int types = factor_types(ctx, nblk);
     uint64_t* part = nullptr;         // per-job-wave mask partials (masks_kernel ORs them)
@@ -1701,11 +1710,11 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     afm::Args a;
     a.T = T;
     a.lda = lda;
-    a.plane = (t1 - t0) * lda;
+    a.plane = (full ? T : t1 - t0) * lda;
     a.close = (const GLB double*)close;
     a.volume = (const GLB double*)volume;
     a.vbits = (const GLB uint64_t*)valid_bits;
-    a.out = (GLB double*)(out - t0 * lda);        // date t's row at a.out + t * lda
+    a.out = (GLB double*)(full ? out : out - t0 * lda);   // date t's row at a.out + t * lda
     a.nanpart = (GLB uint64_t*)part;
     a.badpart = (GLB uint64_t*)(part + afm::kJobSets * nwords * lda);
     a.types = types;
@@ -1747,8 +1756,8 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     if (excess) {                  // NULL: the caller runs afm_labels_f64 (e.g. on another stream)
         dim3 g2((unsigned)((lda + 255) / 256), (unsigned)((t1 - 1) / 64 - t0 / 64 + 1));
         hipLaunchKernelGGL(afm::labels_kernel, g2, dim3(256), 0, ctx->stream, T, t0, t1, lda,
-                           excess, ret1d, valid_bits, out + 96 * a.plane - t0 * lda,
-                           out + 97 * a.plane - t0 * lda);
+                           excess, ret1d, valid_bits, (double*)a.out + 96 * a.plane,
+                           (double*)a.out + 97 * a.plane);
         AFM_HIP(hipGetLastError());
     }
     AFM_HIP(hipFreeAsync(part, ctx->stream));
@@ -1796,6 +1805,25 @@ extern "C" int afm_factors_slab_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t 
                         nanfree_bits, finite_bits, state);
 }
 
+extern "C" int afm_factors_range_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,
+                                     int64_t t1, const double* close, const double* volume,
+                                     const double* ret1d, const double* excess,
+                                     const uint64_t* valid_bits, double* out,
+                                     uint64_t* nanfree_bits, uint64_t* finite_bits, double* state) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && A > 0, "T and A must be positive");
+    AFM_CHECK_ARG(lda >= A && lda % 64 == 0, "lda must be a multiple of 64 and >= A");
+    AFM_CHECK_ARG(close && volume && valid_bits && out && nanfree_bits, "null buffer");
+    AFM_CHECK_ARG((ret1d == nullptr) == (excess == nullptr),
+                  "ret1d and excess are both given or both NULL");
+    AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
+    AFM_CHECK_ARG(0 <= t0 && t0 < t1 && t1 <= T && t0 % 64 == 0 && (t1 % 64 == 0 || t1 == T),
+                  "need 0 <= t0 < t1 <= T with t0 and t1 (unless T) multiples of 64");
+    AFM_CHECK_ARG(state != nullptr, "the slab state buffer is required");
+    return factors_slab(ctx, T, A, lda, t0, t1, close, volume, ret1d, excess, valid_bits, out,
+                        nanfree_bits, finite_bits, state, true);
+}
+
 extern "C" int afm_labels_f64(afm_ctx* ctx, int64_t T, int64_t lda, int64_t t0, int64_t t1,
                               const double* excess, const double* ret1d,
                               const uint64_t* valid_bits, double* target, double* tmr) {
@@ -1819,7 +1847,23 @@ extern "C" int afm_drop_last_obs_bits(afm_ctx* ctx, int64_t T, int64_t lda,
     AFM_CHECK_ARG(T > 0 && lda > 0 && lda % 64 == 0, "bad panel shape");
     AFM_CHECK_ARG(valid_bits && in_bits && out_bits, "null buffer");
     hipLaunchKernelGGL(afm::drop_last_obs_kernel, dim3((unsigned)((lda + 255) / 256)), dim3(256),
-                       0, ctx->stream, (T + 63) / 64, lda, valid_bits, in_bits, out_bits);
+                       0, ctx->stream, (T + 63) / 64, lda, valid_bits, in_bits, out_bits,
+                       (int64_t)0, (T + 63) / 64);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_drop_last_obs_bits_range(afm_ctx* ctx, int64_t T, int64_t lda,
+                                            const uint64_t* valid_bits, const uint64_t* in_bits,
+                                            uint64_t* out_bits, int64_t t0, int64_t t1) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && lda > 0 && lda % 64 == 0, "bad panel shape");
+    AFM_CHECK_ARG(valid_bits && in_bits && out_bits, "null buffer");
+    AFM_CHECK_ARG(0 <= t0 && t0 < t1 && t1 <= T && t0 % 64 == 0 && (t1 % 64 == 0 || t1 == T),
+                  "need 0 <= t0 < t1 <= T with t0 and t1 (unless T) multiples of 64");
+    hipLaunchKernelGGL(afm::drop_last_obs_kernel, dim3((unsigned)((lda + 255) / 256)), dim3(256),
+                       0, ctx->stream, (T + 63) / 64, lda, valid_bits, in_bits, out_bits,
+                       t0 / 64, (t1 + 63) / 64);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

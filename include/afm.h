@@ -89,12 +89,26 @@ int afm_factors_slab_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_
                          const double* ret1d, const double* excess, const uint64_t* valid_bits,
                          double* out, uint64_t* nanfree_bits, uint64_t* finite_bits,
                          double* state);
+/* The same slab written IN PLACE into the whole panel: out [AFM_N_FACTORS][T][lda] and the bit
+ * words [ceil(T/64)][lda] of afm_factors_f64 receive the dates [t0, t1) (t0, and t1 unless it is
+ * T, multiples of 64).  A pipeline can start on the first slab's dates (the z statistics of a
+ * train window) while the next slab builds. */
+int afm_factors_range_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,
+                          int64_t t1, const double* close, const double* volume,
+                          const double* ret1d, const double* excess, const uint64_t* valid_bits,
+                          double* out, uint64_t* nanfree_bits, uint64_t* finite_bits,
+                          double* state);
 
 /* out_bits = in_bits without each asset's last present day (valid_bits): the rows whose
  * shift(-1) labels are NaN.  Used to mask the regression rows up front (the Gram's REDO pass
  * would otherwise re-run those dates). */
 int afm_drop_last_obs_bits(afm_ctx* ctx, int64_t T, int64_t lda, const uint64_t* valid_bits,
                            const uint64_t* in_bits, uint64_t* out_bits);
+/* The same for the words of the dates [t0, t1) only (t0, and t1 unless it is T, multiples of
+ * 64; each asset's last present day still from all T dates). */
+int afm_drop_last_obs_bits_range(afm_ctx* ctx, int64_t T, int64_t lda, const uint64_t* valid_bits,
+                                 const uint64_t* in_bits, uint64_t* out_bits, int64_t t0,
+                                 int64_t t1);
 /* target = excess_ret1d.shift(-1), tmr_ret1d = ret1d.shift(-1) per asset (No-talib.py:90-91) for
  * the grid dates [t0, t1) only (the label planes of afm_factors_f64 for a sub-range; used where
  * the factor panel itself is sharded by asset but the history/PnL planes are needed for every

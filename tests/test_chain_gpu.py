@@ -130,10 +130,13 @@ def test_fama_macbeth_vs_golden(chain_a):
 
 
 @pytest.mark.parametrize("place", [{"labels_side": False}, {"fm_fork": "gram"},
-                                   {"fm_fork": "rebalance"}, {"fm_free_cus": 8}])
+                                   {"fm_fork": "rebalance"}, {"fm_free_cus": 8},
+                                   {"early_zstats": True},
+                                   {"early_zstats": True, "labels_side": False}])
 def test_stream_placement_bit_identical(chain_a, place):
     """The side-stream placements (label planes beside the factor kernel, the FM fork point) move
-    work between streams only: the step's outputs are bitwise those of the default placement."""
+    work between streams only: the step's outputs are bitwise those of the default placement.
+    early_zstats builds the panel in two time slabs with the z statistics between them."""
     import torch
     from afm.pipeline import Pipeline, PipelineConfig
     p, pipe, gold, C = chain_a
@@ -141,7 +144,10 @@ def test_stream_placement_bit_identical(chain_a, place):
                                             window=C["window"], top_n=C["top_n"], **place))
     other.step()
     torch.cuda.synchronize()
-    for name in ("out", "pred", "lasso_beta", "fm_beta"):
+    if place.get("early_zstats"):
+        assert other.early and 0 < other.ta < other.T
+    for name in ("out", "pred", "lasso_beta", "fm_beta", "zs", "nanfree", "finite", "alldf",
+                 "frows", "zrows", "pool_g"):
         a, b = getattr(pipe, name), getattr(other, name)
         assert torch.equal(a.view(torch.int64), b.view(torch.int64)), name
     for k in ("k", "books", "weights"):
