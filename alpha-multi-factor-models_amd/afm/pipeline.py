@@ -117,6 +117,10 @@ class PipelineConfig:
     # (1,280 assets): 8.97 ms per step either way -- the second slab is the ~17 % of dates after
     # the train window, and the z statistics beside it ran 1.69 instead of 1.03 ms -- so off
     early_zstats: bool = False
+    # early_fwd -- one GPU: the analyzer's price rows and forward returns (prediction-independent,
+    # KKT:294-296) on a side stream as soon as the all_df rows exist, beside the z statistics,
+    # instead of at the head of the analyzer stream in the tail
+    early_fwd: bool = True
 
 
 @dataclass
@@ -372,6 +376,7 @@ class Pipeline:
             self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
         self.labels_done = torch.cuda.Event()
+        self.fwd_early = False
         # early z statistics: the first slab ends at the first 64-date boundary past the train
         # window (the slab API's alignment)
         self.ta = min(((sp.tr1 + 63) // 64) * 64, T)
@@ -536,6 +541,13 @@ class Pipeline:
                                              P(self.frows)), "finite rows")
             if not self.early:
                 mark("factors", 1)
+            self.fwd_early = W == 1 and c.analyzer and c.early_fwd
+            if self.fwd_early:
+                self.side2.wait_stream(self.main)                # the all_df rows
+                with torch.cuda.stream(self.side2):
+                    self._analyzer_fwd()
+                h = self.ctx.bind_stream()
+            if not self.early:
                 mark("zstats", 0)
             if self.A_r > 0 and not self.early:
                 if lab_side:
@@ -744,15 +756,11 @@ class Pipeline:
         (KKT:630-631) on the test sub-grid, no host synchronisation."""
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
         full, sp, an = self.full, self.sp, self.an
-        T, lda, a0, Ta = self.T, full.lda, self.an_a0, self.Ta
-        nch = self.nch
+        lda, a0, Ta = full.lda, self.an_a0, self.Ta
         h = self.ctx.bind_stream()
         mark("analyzer", 0)
-        chk(L.afm_row_bits(h, nch, lda, P(self.alldf_full), None, None, sp.s0, T,
-                           P(self.price_bits)), "price rows")
-        cb = a0 // 64
-        chk(L.afm_fwd_returns_f64(h, Ta, lda, P(full.close[a0:]), P(self.price_bits[cb:]),
-                                  P(an["fr"])), "fwd_returns")
+        if not self.fwd_early:
+            self._analyzer_fwd()
         j0, j1 = self.an_rng
         d0 = sp.s0 - a0 + j0                        # sub-grid dates [d0, d1) of this rank
         d1 = d0 + (j1 - j0)
@@ -770,6 +778,18 @@ class Pipeline:
         if self.W > 1:
             return          # the all-gather and the series follow the main chain's exchanges
         self._analyzer_series(mark)
+
+    def _analyzer_fwd(self):
+        """The analyzer's df_test price rows and forward returns (KKT:294-296): they read the close
+        plane and the all_df rows only, not the predictions."""
+        L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+        full, sp, an, a0 = self.full, self.sp, self.an, self.an_a0
+        h = self.ctx.bind_stream()
+        chk(L.afm_row_bits(h, self.nch, full.lda, P(self.alldf_full), None, None, sp.s0, self.T,
+                           P(self.price_bits)), "price rows")
+        cb = a0 // 64
+        chk(L.afm_fwd_returns_f64(h, self.Ta, full.lda, P(full.close[a0:]),
+                                  P(self.price_bits[cb:]), P(an["fr"])), "fwd_returns")
 
     def _analyzer_series(self, mark):
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check

@@ -132,7 +132,8 @@ def test_fama_macbeth_vs_golden(chain_a):
 @pytest.mark.parametrize("place", [{"labels_side": False}, {"fm_fork": "gram"},
                                    {"fm_fork": "rebalance"}, {"fm_free_cus": 8},
                                    {"early_zstats": True},
-                                   {"early_zstats": True, "labels_side": False}])
+                                   {"early_zstats": True, "labels_side": False},
+                                   {"early_fwd": False}])
 def test_stream_placement_bit_identical(chain_a, place):
     """The side-stream placements (label planes beside the factor kernel, the FM fork point) move
     work between streams only: the step's outputs are bitwise those of the default placement.

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """A/B of PipelineConfig switches on the config-C step, each variant in its own process (one
 Pipeline per process: two resident config-C pipelines slow the z-score and Gram stages), run in
-alternation.  Usage: python tools/stage_ab.py [--steps 10 --rounds 2] [--lib-b PATH]
---lib-b: the same config on library variant B (AFM_LIB); without it, the default build alone."""
+alternation.  Usage: python tools/stage_ab.py [--steps 10 --rounds 2] [--lib-b PATH | --cfg-b JSON]
+--lib-b: the same config on library variant B (AFM_LIB); --cfg-a / --cfg-b: two PipelineConfig
+override sets (JSON); without either, the default build alone."""
 import argparse
 import json
 import os
@@ -43,11 +44,15 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--lib-b", default=None)
+    ap.add_argument("--cfg-a", default="{}", help="PipelineConfig overrides of A (JSON)")
+    ap.add_argument("--cfg-b", default=None, help="PipelineConfig overrides of B (JSON)")
     ap.add_argument("--child", default=None)
     a = ap.parse_args()
     if a.child is not None:
         return child(a.child, a.steps)
-    if a.lib_b:
+    if a.cfg_b is not None:
+        variants = {"A": (json.loads(a.cfg_a), None), "B": (json.loads(a.cfg_b), None)}
+    elif a.lib_b:
         variants = {"A": ({}, None), "B": ({}, a.lib_b)}
     else:
         variants = {"default": ({}, None)}
