@@ -56,9 +56,11 @@ __device__ __forceinline__ double div_r(double x, double d, double r) {
 // intercept = y_offset - X_offset . w over the pooled means (shift + G'[0][.] / n).
 constexpr int kLassoThreads = 1024;   // the setup of Q; wave 0 alone runs the descent
 
+// POS: sklearn's positive=True (a launch-time constant: no per-coordinate branch on it)
+template <bool POS>
 __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* gram, int p, double alpha,
                                                       double beta, int max_iter, double tol,
-                                                      int positive, double* w_out, double* info,
+                                                      double* w_out, double* info,
                                                       double alpha_row, const double* shift,
                                                       double* beta_out) {
     extern __shared__ double Q[];                    // [p][p] centered X'X
@@ -96,35 +98,53 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     double rd0 = 1.0 / dd0, rd1 = 1.0 / dd1;
     if (!(__builtin_fabs(rd0) > 0x1p-400 && __builtin_fabs(rd0) < 0x1p400)) rd0 = 0.0;
     if (!(__builtin_fabs(rd1) > 0x1p-400 && __builtin_fabs(rd1) < 0x1p400)) rd1 = 0.0;
-    const bool all_rd = __ballot((has0 && rd0 == 0.0) || (has1 && rd1 == 0.0)) == 0ull;
-    auto movable = [&](double qd, double q, double h, double w) {
+    // lanes whose coordinate exists and can ever move (a zero diagonal never moves)
+    const uint64_t live0 = __ballot(has0 && qd0 != 0.0), live1 = __ballot(has1 && qd1 != 0.0);
+    // movable now (with its nonzero diagonal): w != 0, or the soft threshold of q - h is nonzero
+    // -- fmax(|t| - alpha, 0) != 0 is |t| > alpha (t - alpha = 0 only at t = alpha; NaN: false)
+    auto moves = [&](double q, double h, double w) {
         const double tmp = q - h;
-        const bool nz = (positive && tmp < 0) ? false : __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0) != 0.0;
-        return qd != 0.0 && (w != 0.0 || nz);
+        return w != 0.0 || (POS ? tmp > alpha : __builtin_fabs(tmp) > alpha);
     };
     // the signed zero the skipped coordinate would store: fsign(tmp) * 0 / (qii + beta)
     auto zero_of = [&](double q, double h) {
         const double tmp = q - h;
-        return (positive && tmp < 0) ? 0.0 : (tmp < 0 ? -0.0 : 0.0);
+        return (POS && tmp < 0) ? 0.0 : (tmp < 0 ? -0.0 : 0.0);
+    };
+    // per-coordinate constants (q_j = X'y, the diagonal, its reciprocal) in LDS: the step reads
+    // them as broadcast loads beside the row instead of v_readlane picks
+    __shared__ double cq[kMaxLassoP], cqd[kMaxLassoP], crd[kMaxLassoP];
+    if (has0) { cq[j0] = q0; cqd[j0] = qd0; crd[j0] = rd0; }
+    if (has1) { cq[j1] = q1; cqd[j1] = qd1; crd[j1] = rd1; }
+    // lanes [lo, hi) of a half (lo, hi in 0..64) as a mask
+    auto span = [](int lo, int hi) -> uint64_t {
+        lo = lo < 0 ? 0 : (lo > 64 ? 64 : lo);
+        hi = hi < 0 ? 0 : (hi > 64 ? 64 : hi);
+        if (hi <= lo) return 0ull;
+        const uint64_t up = hi == 64 ? ~0ull : ((1ull << hi) - 1ull);
+        return up & ~((1ull << lo) - 1ull);
     };
     for (n_iter = 0; n_iter < max_iter; ++n_iter) {
         double w_max = 0.0, d_w_max = 0.0;
         for (int ii = 0; ii < p; ++ii) {
             {   // skip coordinates [ii, next) that cannot move (exactly sklearn's no-ops)
-                const uint64_t m0 = __ballot(has0 && j0 >= ii && movable(qd0, q0, h0, w0));
-                const uint64_t m1 = __ballot(has1 && j1 >= ii && movable(qd1, q1, h1, w1));
-                const int next = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : p);
-                if (next > ii) {
-                    if (has0 && j0 >= ii && j0 < next && qd0 != 0.0) w0 = zero_of(q0, h0);
-                    if (has1 && j1 >= ii && j1 < next && qd1 != 0.0) w1 = zero_of(q1, h1);
-                    ii = __builtin_amdgcn_readfirstlane(next);
+                const uint64_t m0 = __builtin_amdgcn_ballot_w64(moves(q0, h0, w0)) & live0 & span(ii, 64);
+                const uint64_t m1 = __builtin_amdgcn_ballot_w64(moves(q1, h1, w1)) & live1 &
+                                    span(ii - 64, 64);
+                const int next = __builtin_amdgcn_readfirstlane(
+                    m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : p));
+                if (next > ii) {                    // (uniform) their stored signed zeros
+                    const uint64_t z0 = live0 & span(ii, next), z1 = live1 & span(ii - 64, next - 64);
+                    if (__builtin_amdgcn_inverse_ballot_w64(z0)) w0 = zero_of(q0, h0);
+                    if (__builtin_amdgcn_inverse_ballot_w64(z1)) w1 = zero_of(q1, h1);
+                    ii = next;
                     if (ii >= p) break;
                 }
             }
             // (the ballot above never stops at a coordinate with a zero diagonal: not movable)
             const double* row = Q + ii * p;
             const double r0 = has0 ? row[j0] : 0.0, r1 = has1 ? row[j1] : 0.0;
-            const double qii = pick(qd0, qd1, ii);
+            const double qii = cqd[ii];
             const double w_ii = pick(w0, w1, ii);
             // H[ii] after the first axpy is lane ii's own fma (r = Q[ii][ii] there): computed on
             // the scalar path directly, so the step does not wait for the row read or the axpy
@@ -135,18 +155,15 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
             // only through q - h and further fmas)
             h0 = __builtin_fma(-w_ii, r0, h0);
             h1 = __builtin_fma(-w_ii, r1, h1);
-            const double tmp = pick(q0, q1, ii) - hh;
+            const double tmp = cq[ii] - hh;
             double wn;
-            if (positive && tmp < 0) {
+            if (POS && tmp < 0) {
                 wn = 0.0;
             } else {
+                // (a divisor without a normal reciprocal has rd = 0: q0 = 0 takes div_r's IEEE
+                // branch)
                 const double num = fsign(tmp) * __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0);
-                if (all_rd) {
-                    wn = div_r(num, qii + beta, pick(rd0, rd1, ii));
-                } else {
-                    const double rdi = pick(rd0, rd1, ii);
-                    wn = rdi != 0.0 ? div_r(num, qii + beta, rdi) : num / (qii + beta);
-                }
+                wn = div_r(num, qii + beta, crd[ii]);
             }
             w0 = lane == ii ? wn : w0;
             w1 = lane + 64 == ii ? wn : w1;
@@ -162,7 +179,7 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
                 const double wj = pick(w0, w1, j), qj = pick(q0, q1, j), hj = pick(h0, h1, j);
                 q_dot_w = q_dot_w + wj * qj;
                 const double xta = qj - hj - beta * wj;
-                const double a = positive ? xta : __builtin_fabs(xta);
+                const double a = POS ? xta : __builtin_fabs(xta);
                 if (j == 0 || a > dual) dual = a;
                 wh = wh + wj * hj;
                 w_norm2 = w_norm2 + wj * wj;
@@ -205,6 +222,27 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
 }  // namespace
 }  // namespace afm
 
+template <bool POS>
+static int launch_cd_t(afm_ctx* ctx, int lds, const double* gram, int p, double alpha, double beta,
+                       int max_iter, double tol, double* w, double* info, double alpha_row,
+                       const double* shift, double* beta_out) {
+    AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::lasso_cd_kernel<POS>,
+                           (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
+    hipLaunchKernelGGL(afm::lasso_cd_kernel<POS>, dim3(1), dim3(afm::kLassoThreads), lds,
+                       ctx->stream, gram, p, alpha, beta, max_iter, tol, w, info, alpha_row, shift,
+                       beta_out);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+static int launch_cd(afm_ctx* ctx, bool positive, int lds, const double* gram, int p, double alpha,
+                     double beta, int max_iter, double tol, double* w, double* info,
+                     double alpha_row, const double* shift, double* beta_out) {
+    return positive ? launch_cd_t<true>(ctx, lds, gram, p, alpha, beta, max_iter, tol, w, info,
+                                        alpha_row, shift, beta_out)
+                    : launch_cd_t<false>(ctx, lds, gram, p, alpha, beta, max_iter, tol, w, info,
+                                         alpha_row, shift, beta_out);
+}
+
 extern "C" int afm_lasso_cd_f64(afm_ctx* ctx, const double* gram, int p, double alpha_n,
                                 double beta, int max_iter, double tol, int positive, double* w,
                                 double* info) {
@@ -214,12 +252,8 @@ extern "C" int afm_lasso_cd_f64(afm_ctx* ctx, const double* gram, int p, double 
     AFM_CHECK_ARG(max_iter >= 1, "max_iter must be >= 1");
     AFM_CHECK_ARG(alpha_n >= 0 && beta >= 0 && tol >= 0, "alpha, beta and tol must be >= 0");
     const int lds = (int)sizeof(double) * p * p;
-    AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::lasso_cd_kernel, (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
-    hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(afm::kLassoThreads), lds, ctx->stream,
-                       gram, p, alpha_n, beta, max_iter, tol, positive, w, info, -1.0,
-                       (const double*)nullptr, (double*)nullptr);
-    AFM_HIP(hipGetLastError());
-    return AFM_OK;
+    return launch_cd(ctx, positive != 0, lds, gram, p, alpha_n, beta, max_iter, tol, w, info, -1.0,
+                     nullptr, nullptr);
 }
 
 extern "C" int afm_lasso_fit_f64(afm_ctx* ctx, const double* gram, const double* shift, int p,
@@ -230,10 +264,6 @@ extern "C" int afm_lasso_fit_f64(afm_ctx* ctx, const double* gram, const double*
     AFM_CHECK_ARG(gram && shift && beta_out && info, "null buffer");
     AFM_CHECK_ARG(max_iter >= 1 && alpha >= 0 && tol >= 0, "bad max_iter / alpha / tol");
     const int lds = (int)sizeof(double) * p * p;
-    AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::lasso_cd_kernel, (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
-    hipLaunchKernelGGL(afm::lasso_cd_kernel, dim3(1), dim3(afm::kLassoThreads), lds, ctx->stream,
-                       gram, p, 0.0, 0.0, max_iter, tol, positive, (double*)nullptr, info, alpha, shift,
-                       beta_out);
-    AFM_HIP(hipGetLastError());
-    return AFM_OK;
+    return launch_cd(ctx, positive != 0, lds, gram, p, 0.0, 0.0, max_iter, tol, nullptr, info, alpha,
+                     shift, beta_out);
 }
