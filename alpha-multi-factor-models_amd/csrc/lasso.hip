@@ -23,6 +23,7 @@ namespace afm {
 namespace {
 
 constexpr int kMaxLassoP = 110;
+constexpr int kQS = 128;                 // LDS row stride of Q (doubles): lanes j and j + 64
 
 __device__ __forceinline__ double bcast(double v, int lane) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
@@ -63,16 +64,16 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
                                                       double* w_out, double* info,
                                                       double alpha_row, const double* shift,
                                                       double* beta_out) {
-    extern __shared__ double Q[];                    // [p][p] centered X'X
+    extern __shared__ double Q[];                    // [p][kQS] centered X'X, zero past column p
     const int tid = threadIdx.x, lane = tid & 63;
     const int p2 = p + 2;
     const double n = gram[0];
     if (alpha_row >= 0.0) alpha = alpha_row * n;
     // centered moments C = G'[1:,1:] - (g0 g0^T) / n of [x, y] (oracle.centered_moments), by the
     // whole block: a lone wave took ~150 dependent rounds of L2 loads and a division here
-    for (int e = tid; e < p * p; e += kLassoThreads) {
-        const int i = e / p, j = e - i * p;
-        Q[e] = gram[(1 + i) * p2 + 1 + j] - (gram[1 + i] * gram[1 + j]) / n;
+    for (int e = tid; e < p * kQS; e += kLassoThreads) {
+        const int i = e / kQS, j = e - i * kQS;
+        Q[e] = j < p ? gram[(1 + i) * p2 + 1 + j] - (gram[1 + i] * gram[1 + j]) / n : 0.0;
     }
     __syncthreads();
     if (tid >= 64) return;
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     // per-lane diagonal: a coordinate whose weight is 0 and whose soft threshold gives 0 again
     // changes nothing (no H update, w stays a signed zero) -- the sweep skips to the next
     // coordinate that can move, found by ballot over the lanes' current H
-    const double qd0 = has0 ? Q[j0 * p + j0] : 0.0, qd1 = has1 ? Q[j1 * p + j1] : 0.0;
+    const double qd0 = has0 ? Q[j0 * kQS + j0] : 0.0, qd1 = has1 ? Q[j1 * kQS + j1] : 0.0;
     // the soft-threshold divisors qii + beta and their correctly rounded reciprocals (a divisor
     // whose reciprocal is not normal keeps the IEEE division: rd = 0 marks it)
     const double dd0 = qd0 + beta, dd1 = qd1 + beta;
@@ -102,9 +103,11 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     const uint64_t live0 = __ballot(has0 && qd0 != 0.0), live1 = __ballot(has1 && qd1 != 0.0);
     // movable now (with its nonzero diagonal): w != 0, or the soft threshold of q - h is nonzero
     // -- fmax(|t| - alpha, 0) != 0 is |t| > alpha (t - alpha = 0 only at t = alpha; NaN: false)
-    auto moves = [&](double q, double h, double w) {
+    // (two ballots of plain compares: the lane masks go straight to SGPRs)
+    auto moves = [&](double q, double h, double w) -> uint64_t {
         const double tmp = q - h;
-        return w != 0.0 || (POS ? tmp > alpha : __builtin_fabs(tmp) > alpha);
+        return __builtin_amdgcn_ballot_w64(w != 0.0) |
+               __builtin_amdgcn_ballot_w64(POS ? tmp > alpha : __builtin_fabs(tmp) > alpha);
     };
     // the signed zero the skipped coordinate would store: fsign(tmp) * 0 / (qii + beta)
     auto zero_of = [&](double q, double h) {
@@ -128,9 +131,8 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
         double w_max = 0.0, d_w_max = 0.0;
         for (int ii = 0; ii < p; ++ii) {
             {   // skip coordinates [ii, next) that cannot move (exactly sklearn's no-ops)
-                const uint64_t m0 = __builtin_amdgcn_ballot_w64(moves(q0, h0, w0)) & live0 & span(ii, 64);
-                const uint64_t m1 = __builtin_amdgcn_ballot_w64(moves(q1, h1, w1)) & live1 &
-                                    span(ii - 64, 64);
+                const uint64_t m0 = moves(q0, h0, w0) & live0 & span(ii, 64);
+                const uint64_t m1 = moves(q1, h1, w1) & live1 & span(ii - 64, 64);
                 const int next = __builtin_amdgcn_readfirstlane(
                     m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : p));
                 if (next > ii) {                    // (uniform) their stored signed zeros
@@ -142,8 +144,8 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
                 }
             }
             // (the ballot above never stops at a coordinate with a zero diagonal: not movable)
-            const double* row = Q + ii * p;
-            const double r0 = has0 ? row[j0] : 0.0, r1 = has1 ? row[j1] : 0.0;
+            const double* row = Q + ii * kQS;          // (zero past column p: no lane masks)
+            const double r0 = row[j0], r1 = row[j1];
             const double qii = cqd[ii];
             const double w_ii = pick(w0, w1, ii);
             // H[ii] after the first axpy is lane ii's own fma (r = Q[ii][ii] there): computed on
@@ -227,7 +229,7 @@ static int launch_cd_t(afm_ctx* ctx, int lds, const double* gram, int p, double 
                        int max_iter, double tol, double* w, double* info, double alpha_row,
                        const double* shift, double* beta_out) {
     AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::lasso_cd_kernel<POS>,
-                           (int)sizeof(double) * afm::kMaxLassoP * afm::kMaxLassoP));
+                           (int)sizeof(double) * afm::kMaxLassoP * afm::kQS));
     hipLaunchKernelGGL(afm::lasso_cd_kernel<POS>, dim3(1), dim3(afm::kLassoThreads), lds,
                        ctx->stream, gram, p, alpha, beta, max_iter, tol, w, info, alpha_row, shift,
                        beta_out);
@@ -251,7 +253,7 @@ extern "C" int afm_lasso_cd_f64(afm_ctx* ctx, const double* gram, int p, double 
     AFM_CHECK_ARG(gram && w && info, "null buffer");
     AFM_CHECK_ARG(max_iter >= 1, "max_iter must be >= 1");
     AFM_CHECK_ARG(alpha_n >= 0 && beta >= 0 && tol >= 0, "alpha, beta and tol must be >= 0");
-    const int lds = (int)sizeof(double) * p * p;
+    const int lds = (int)sizeof(double) * p * afm::kQS;
     return launch_cd(ctx, positive != 0, lds, gram, p, alpha_n, beta, max_iter, tol, w, info, -1.0,
                      nullptr, nullptr);
 }
@@ -263,7 +265,7 @@ extern "C" int afm_lasso_fit_f64(afm_ctx* ctx, const double* gram, const double*
     AFM_CHECK_ARG(p >= 1 && p <= afm::kMaxLassoP, "need 1 <= p <= 110");
     AFM_CHECK_ARG(gram && shift && beta_out && info, "null buffer");
     AFM_CHECK_ARG(max_iter >= 1 && alpha >= 0 && tol >= 0, "bad max_iter / alpha / tol");
-    const int lds = (int)sizeof(double) * p * p;
+    const int lds = (int)sizeof(double) * p * afm::kQS;
     return launch_cd(ctx, positive != 0, lds, gram, p, 0.0, 0.0, max_iter, tol, nullptr, info, alpha,
                      shift, beta_out);
 }
