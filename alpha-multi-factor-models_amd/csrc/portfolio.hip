@@ -1731,12 +1731,17 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                                                       double* turnover, double* long_ret,
                                                       double* short_ret, const int32_t* idx) {
     __shared__ int buf[2][kBufWords];
-    __shared__ int offs[2][kChunkDates];
     __shared__ double sm[2][kChunkDates + 1][4];
     __shared__ double rcp[2][kChunkDates + 1][2];           // RN(1 / S[2]), RN(1 / S[3])
     __shared__ int64_t cstart[2];
     __shared__ int ccount[2];
     __shared__ double node[2 * kMaxTerms];
+    // per staged date, derived by the loader from its record: {offset, m, nint, L}, each lane's
+    // leaf code (lanes < m) and dataflow descriptor (lanes < nint) -- so the scan reads a date's
+    // inputs with independent loads (one LDS round trip) instead of a chain through the record
+    __shared__ int4 hdr[2][kChunkDates];
+    __shared__ unsigned char code8[2][kChunkDates][64];
+    __shared__ int wdv[2][kChunkDates][64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t base = (int64_t)blockIdx.x * nd;
     rec += base * kRec;
@@ -1759,7 +1764,6 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
         const bool fits = (i0 + lane < nd) && incl <= kBufWords;
         const u64 fm = __ballot(fits);
         const int c = fm == ~0ull ? 64 : __builtin_ctzll(~fm);   // prefix of dates that fits
-        if (lane < c) offs[b][lane] = incl - len;
         // the records' first 128 words for 16 dates at a time, every load issued before the LDS
         // writes (round 4: a date-by-date copy waited one global-load latency per date, ~1 us,
         // and the scan waited for it at the chunk barrier); longer records' tails after
@@ -1789,6 +1793,14 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
             if (l <= 128) continue;                                  // (uniform)
             const int32_t* src = rec + (i0 + j) * kRec;
             for (int e = 128 + lane; e < l; e += 64) buf[b][o + e] = src[e];
+        }
+        for (int j = 0; j < c; ++j) {            // (this wave's own LDS writes: in order)
+            const int o = __shfl(incl - len, j, 64);
+            const int* R = &buf[b][o];
+            const int m = R[0], nint = R[1], L = R[2];
+            code8[b][j][lane] = (unsigned char)(lane < m ? R[4 + lane] : 0);
+            wdv[b][j][lane] = m > 0 && lane < nint ? R[4 + m + lane] : 0;
+            if (lane == 0) hdr[b][j] = make_int4(o, m, nint, L);
         }
         constexpr int kSumIt = ((kChunkDates + 1) * 4 + 63) / 64;   // all loads first
         double sv[kSumIt];
@@ -1830,25 +1842,23 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
             // date j's V-independent inputs, read one date ahead
             struct Pre {
                 const int* R;
-                int m, nint, L, code, en0, w0, wd;
+                int m, nint, L, code, wd;
                 double s0, s1, s2, s3, r2, r3;
             };
-            auto prefetch = [&](int j) {
+            auto prefetch = [&](int j) {         // independent loads only (see hdr)
                 Pre f;
-                f.R = &buf[b][offs[b][j]];
-                f.m = f.R[0];
-                f.nint = f.R[1];
-                f.L = f.R[2];
+                const int4 hd = hdr[b][j];
+                f.R = &buf[b][hd.x];
+                f.m = hd.y;
+                f.nint = hd.z;
+                f.L = hd.w;
                 const double* S = sm[b][j + 1];
                 f.s0 = S[0]; f.s1 = S[1]; f.s2 = S[2]; f.s3 = S[3];
                 f.r2 = rcp[b][j + 1][0];
                 f.r3 = rcp[b][j + 1][1];
-                f.code = lane < f.m ? f.R[4 + lane] : 0;
-                const int* lend = f.R + 4 + (f.m > 0 ? f.m : 0) + f.nint;
-                f.en0 = f.m > 0 && f.L > 0 ? lend[0] : 0;
-                f.w0 = lane < f.en0 ? f.R[4 + f.m + lane] : 0;
+                f.code = code8[b][j][lane];
                 // the dataflow evaluation's descriptor (internal node `lane`, level order)
-                f.wd = f.m > 0 && lane < f.nint ? f.R[4 + f.m + lane] : 0;
+                f.wd = wdv[b][j][lane];
                 return f;
             };
             Pre cur = prefetch(0);
@@ -1893,8 +1903,8 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                         // one DAG level per step, no lgkmcnt(0) wait (see above); the next level's
                         // first add descriptor is fetched while this level's node reads are in flight
                         int st = 0;
-                        int en = f.en0;
-                        int wcur = f.w0;
+                        int en = L > 0 ? lend[0] : 0;
+                        int wcur = lane < en ? adds[lane] : 0;
                         for (int l = 0; l < L; ++l) {
                             const int en2 = l + 1 < L ? lend[l + 1] : en;
                             const int wnext = en + lane < en2 ? adds[en + lane] : 0;

@@ -41,6 +41,10 @@ def main():
         torch.cuda.synchronize()
         ts.append(ev[0].elapsed_time(ev[1]))
     us = pipe.reb["usize"].cpu().numpy()
+    import hashlib
+    dig = hashlib.sha1(q["value"].cpu().numpy().tobytes() +
+                       q["turnover"].cpu().numpy().tobytes()).hexdigest()[:12]
+    print(f"lib={os.environ.get('AFM_LIB') or 'default'} value+turnover {dig}")
     print(f"A={a.assets} dates={pipe.nd}: afm_pnl_scan_f64 alone {np.median(ts):.3f} ms "
           f"(min {min(ts):.3f}) = {np.median(ts) * 1e3 / pipe.nd:.2f} us per date; union size "
           f"median {int(np.median(us[:, 0]))}, max {int(us[:, 0].max())}", flush=True)
