@@ -1741,7 +1741,11 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
     // inputs with independent loads (one LDS round trip) instead of a chain through the record
     __shared__ int4 hdr[2][kChunkDates];
     __shared__ unsigned char code8[2][kChunkDates][64];
-    __shared__ int wdv[2][kChunkDates][64];
+    __shared__ unsigned gdv[2][kChunkDates][64];
+    // two-level dataflow (DAGs of <= 64 adds): lane q's grandchildren ids, 8 bits each (ids <=
+    // 129 there); a leaf child c reads as (c, kZ), node[kZ] = -0.0, the exact additive identity
+    // (x + -0 = x for every x, +0 and -0 included)
+    constexpr int kZ = 255;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t base = (int64_t)blockIdx.x * nd;
     rec += base * kRec;
@@ -1799,7 +1803,15 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
             const int* R = &buf[b][o];
             const int m = R[0], nint = R[1], L = R[2];
             code8[b][j][lane] = (unsigned char)(lane < m ? R[4 + lane] : 0);
-            wdv[b][j][lane] = m > 0 && lane < nint ? R[4 + m + lane] : 0;
+            unsigned g = 0u;
+            if (m > 0 && nint <= 64 && lane < nint) {
+                const int wd = R[4 + m + lane], c0 = wd & 0xffff, c1 = wd >> 16;
+                const int ga = c0 >= m ? R[4 + c0] : (c0 | (kZ << 16));
+                const int gb = c1 >= m ? R[4 + c1] : (c1 | (kZ << 16));
+                g = (unsigned)(ga & 0xff) | (unsigned)((ga >> 16) & 0xff) << 8 |
+                    (unsigned)(gb & 0xff) << 16 | (unsigned)((gb >> 16) & 0xff) << 24;
+            }
+            gdv[b][j][lane] = g;
             if (lane == 0) hdr[b][j] = make_int4(o, m, nint, L);
         }
         constexpr int kSumIt = ((kChunkDates + 1) * 4 + 63) / 64;   // all loads first
@@ -1842,7 +1854,8 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
             // date j's V-independent inputs, read one date ahead
             struct Pre {
                 const int* R;
-                int m, nint, L, code, wd;
+                int m, nint, L, code;
+                unsigned gd;
                 double s0, s1, s2, s3, r2, r3;
             };
             auto prefetch = [&](int j) {         // independent loads only (see hdr)
@@ -1857,8 +1870,8 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                 f.r2 = rcp[b][j + 1][0];
                 f.r3 = rcp[b][j + 1][1];
                 f.code = code8[b][j][lane];
-                // the dataflow evaluation's descriptor (internal node `lane`, level order)
-                f.wd = wdv[b][j][lane];
+                // the dataflow evaluation's grandchildren (internal node `lane`, level order)
+                f.gd = gdv[b][j][lane];
                 return f;
             };
             Pre cur = prefetch(0);
@@ -1884,13 +1897,16 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                     if (lane < m) node[lane] = leaf(f.code);
                     for (int e = lane + 64; e < m; e += 64) node[e] = leaf(R[4 + e]);
                     if (nint <= 64 && nint > 0) {
-                        // dataflow: lane q recomputes internal node q from the current node
-                        // values L times (a node of level h is final after h passes); the
-                        // descriptors were read a date ahead, the root stays in its lane's register
-                        const int a0 = f.wd & 0xffff, b0 = f.wd >> 16;
+                        // dataflow: lane q recomputes internal node q from its grandchildren's
+                        // current values, (gaa + gab) + (gba + gbb) -- the additions its children's
+                        // lanes make -- ceil(L / 2) times (a node of height h is final after
+                        // ceil(h / 2) passes); the root stays in its lane's register
+                        const int aa = f.gd & 0xff, ab = (f.gd >> 8) & 0xff;
+                        const int ba = (f.gd >> 16) & 0xff, bb = f.gd >> 24;
+                        if (lane == 0) node[kZ] = -0.0;      // (the level path may reuse it)
                         double v = 0.0;
-                        for (int l = 0; l < L; ++l) {
-                            v = node[a0] + node[b0];
+                        for (int l = 0; l < L; l += 2) {
+                            v = (node[aa] + node[ab]) + (node[ba] + node[bb]);
                             if (lane < nint) node[m + lane] = v;
                         }
                         const uint64_t rb = __builtin_bit_cast(uint64_t, v);

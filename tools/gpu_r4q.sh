@@ -1,5 +1,5 @@
 #!/bin/bash
-# PnL scan: per-date inputs derived by the loader wave (product) vs read through the record (pbase); portfolio / chain / config tests
+# PnL scan: two-level dataflow on loader-derived grandchildren (product) vs one level (pbase); portfolio / chain / config tests
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; o=gpurun_out/r4q; mkdir -p $o
 P=$R/alpha-multi-factor-models_amd/build/exp
