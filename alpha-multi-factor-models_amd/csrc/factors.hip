@@ -1075,7 +1075,7 @@ struct Pack<H, R...> {
 // (6-7 moving sums / bands) at positions 1, 3, the SIMDs the loaders share.  Config C: the same
 // time as the round-3 partition (10.3-10.7 ms, the kernel is bound by its write stream there);
 // at 1,250 assets, where each set runs alone on its SIMD (the 15-way split), 4.06 vs 4.30-4.54 ms
-// -- the correlations no longer share a wave (tools/gpu_r4i.sh, profiles/r4_i_partition_ab.txt).
+// -- the correlations no longer share a wave (tools/archive/gpu_r4i.sh, profiles/r4_i_partition_ab.txt).
 // A variant that moved one moving sum from each heavy set to a light one ran slower at both
 // sizes (11.0 / 4.7 ms).  The heavy sets' fast steps keep <= 8 scratch accesses (slab entry
 // reloads; the day loop's chains have none).

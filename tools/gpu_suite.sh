@@ -1,7 +1,7 @@
 #!/bin/bash
-# full GPU suite + bench line + per-rank proxy + PnL alone
+# full GPU suite + bench line + per-rank proxy + PnL alone (round-4 run r4h)
 set -o pipefail
-R=$GRAFT_REPO_ROOT; cd $R; o=gpurun_out/r4h; mkdir -p $o
+R=$GRAFT_REPO_ROOT; cd $R; o=gpurun_out/suite; mkdir -p $o
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > $o/tests.log 2>&1
 rc=$?; tail -2 $o/tests.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error" $o/tests.log | head -20; exit 1; }
 timeout -k 10 300 python -u tools/pnl_probe.py > $o/pnl.txt 2>&1 || { tail -5 $o/pnl.txt; exit 1; }
