@@ -759,43 +759,85 @@ __global__ __launch_bounds__(128) void xs_stats_kernel(StatArgs g) {
     int lcnt = 0;
     for (int c0 = 0; c0 < n; c0 += kStatRows) {
         const int len = min(kStatRows, n - c0);
+        // the chunk's loads, all issued before any LDS write (round 4: a row-by-row copy waited
+        // one global-load latency per row of each thread, and the whole per-date kernel was that
+        // wait: 0.55 ms per date with or without the sequential lanes)
+        constexpr int kPer = kStatRows / 128;
+        double lv[kPer][4];
+        int lra[kPer], lrd[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int e = tid + 128 * u;
+            const int64_t o = base + c0 + (e < len ? e : 0);
+            lv[u][0] = g.rows[o];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) lv[u][1 + q] = g.rows[(1 + q) * plane + o];
+            lra[u] = g.rank_asc[o];
+            lrd[u] = g.rank_desc[o];
+        }
         __syncthreads();                                   // the previous chunk is consumed
-        for (int e = tid; e < len; e += 128) {
-            const int64_t o = base + c0 + e;
-            sv[0][e] = g.rows[o];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int e = tid + 128 * u;
+            if (e >= len) continue;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sv[q][e] = lv[u][q];
             sinv[e] = 1. / (double)(c0 + e + 1);
-            for (int q = 0; q < 3; ++q) sv[1 + q][e] = g.rows[(1 + q) * plane + o];
-            const double pct = (double)g.rank_asc[o] / (double)n;     // KKT:328-330
+            const double pct = (double)lra[u] / (double)n;              // KKT:328-330
             int layer = (int)(pct * kLayers) + 1;
             if (layer > kLayers) layer = kLayers;
             slay[e] = (int8_t)(layer - 1);
-            const int rd = g.rank_desc[o];
+            const int rd = lrd[u];
             if (rd <= kTopK) {
-                pv_f[rd - 1] = sv[0][e];
-                for (int q = 0; q < 3; ++q) pv_r[q][rd - 1] = sv[1 + q][e];
+                pv_f[rd - 1] = lv[u][0];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) pv_r[q][rd - 1] = lv[u][1 + q];
                 pv_has[rd - 1] = 1;
             }
         }
         // one flag for the chunk: every staged value finite (the analyzer's rows always are)
         int fin = 1;
-        for (int e = tid; e < len; e += 128)
-            fin &= __builtin_isfinite(sv[0][e]) && __builtin_isfinite(sv[1][e]) &&
-                   __builtin_isfinite(sv[2][e]) && __builtin_isfinite(sv[3][e]);
+#pragma unroll
+        for (int u = 0; u < kPer; ++u)
+            if (tid + 128 * u < len)
+                fin &= __builtin_isfinite(lv[u][0]) && __builtin_isfinite(lv[u][1]) &&
+                       __builtin_isfinite(lv[u][2]) && __builtin_isfinite(lv[u][3]);
         const bool all_fin = __syncthreads_and(fin);
         if (wave == 0 && lane < 3) {
             const double* R = sv[1 + k0];
             if (all_fin && nobs == (double)c0) {
-                // no row skipped so far: nobs == row number, 1 / nobs from the table, no branch
-#pragma unroll 4
-                for (int e = 0; e < len; ++e) {
-                    const double vy = sv[0][e], vx = R[e], inv = sinv[e];
+                // no row skipped so far: nobs == row number, 1 / nobs from the table, no branch.
+                // Blocks of 8 rows whose LDS values were read during the previous block (the
+                // recurrences' chain -- sub, mul, add per row -- never waits for LDS), the tail
+                // row by row
+                auto step = [&](double vy, double vx, double inv) {
                     const double dx = vx - mx, dy = vy - my;
                     mx += inv * dx;
                     my += inv * dy;
                     sxx += (vx - mx) * dx;
                     syy += (vy - my) * dy;
                     sxy += (vx - mx) * dy;
+                };
+                constexpr int kB = 8;
+                const int nb = len / kB;
+                double ny[kB], nx[kB], ni[kB];
+                if (nb > 0) {
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) { ny[u] = sv[0][u]; nx[u] = R[u]; ni[u] = sinv[u]; }
                 }
+                for (int b = 0; b < nb; ++b) {
+                    double y[kB], x[kB], iv[kB];
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) { y[u] = ny[u]; x[u] = nx[u]; iv[u] = ni[u]; }
+                    const int e1 = (b + 1 < nb ? b + 1 : b) * kB;   // (the last block re-reads)
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) {
+                        ny[u] = sv[0][e1 + u]; nx[u] = R[e1 + u]; ni[u] = sinv[e1 + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kB; ++u) step(y[u], x[u], iv[u]);
+                }
+                for (int e = nb * kB; e < len; ++e) step(sv[0][e], R[e], sinv[e]);
                 nobs += (double)len;
             } else {
                 for (int e = 0; e < len; ++e) {

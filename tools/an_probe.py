@@ -40,6 +40,11 @@ def main():
                                                P(an["rows"]), P(an["nrows"]), P(an["ra"]),
                                                P(an["rd"]), 10, P(an["ic"]), P(an["layer_mean"]),
                                                P(an["layer_cnt"]), P(an["port"])),
+        "xs_stats_76dates": lambda: L.afm_xs_stats_f64(h, Ta, lda, P(pipe.an_dates), 76,
+                                                       P(an["rows"]), P(an["nrows"]), P(an["ra"]),
+                                                       P(an["rd"]), 10, P(an["ic"]),
+                                                       P(an["layer_mean"]), P(an["layer_cnt"]),
+                                                       P(an["port"])),
         "xs_series": lambda: L.afm_xs_series_f64(h, pipe.an_nd, P(an["layer_mean"]), P(an["port"]),
                                                  P(an["ic"]), P(pipe.an_year), pipe.an_nyears,
                                                  pipe.an_year0, P(an["cum_layer"]), P(an["ls"]),
@@ -62,6 +67,12 @@ def main():
             torch.cuda.synchronize()
             ts.append(ev[0].elapsed_time(ev[1]))
         print(f"{name}: {np.median(ts) * 1e3:.1f} us", flush=True)
+        if name == "xs_stats":
+            import hashlib
+            dig = hashlib.sha1(an["ic"].cpu().numpy().tobytes() +
+                               an["layer_mean"].cpu().numpy().tobytes() +
+                               an["port"].cpu().numpy().tobytes()).hexdigest()[:12]
+            print(f"lib={os.environ.get('AFM_LIB') or 'default'} xs_stats outputs {dig}", flush=True)
 
 
 if __name__ == "__main__":
