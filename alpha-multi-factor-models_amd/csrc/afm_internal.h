@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <unordered_map>
 
 #include "afm.h"
 
@@ -18,6 +19,9 @@ struct afm_ctx {
     int factor_pair = 1;     // 3-way split: two items per workgroup
     int factor_fast = 1;     // clean-window fast step on
     int gram_checked = 0;    // afm_xs_gram_f64: checked staging only (no FAST + REDO passes)
+    // factor slab calls: the work split each state buffer's layout was written with (the state
+    // is [block][split][wave]; a later slab under another factor_split would misread it)
+    std::unordered_map<const void*, int> slab_types;
 };
 
 void afm_set_error(const std::string& msg);

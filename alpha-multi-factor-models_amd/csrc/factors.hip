@@ -1698,6 +1698,19 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     // full: out / nanfree / finite are the whole [T]-date panel and bit words (the slab's rows
     // and words written in place); else they hold the slab's dates only
     const int64_t nwords = (t1 - t0 + 63) / 64;                   // the slab's mask words
+    if (state) {                     // the state layout depends on the split: keep it per series
+        const int types_now = factor_types(ctx, (A + 63) / 64);
+        if (t0 == 0) {
+            ctx->slab_types[state] = types_now;
+        } else {
+            const auto it = ctx->slab_types.find(state);
+            if (it != ctx->slab_types.end() && it->second != types_now) {
+                afm_set_error("factor slab: factor_split changed between slabs of one series "
+                              "(the carried state was written under another split)");
+                return AFM_E_ARG;
+            }
+        }
+    }
     if (full) {
         nanfree_bits += (t0 / 64) * lda;
         if (finite_bits) finite_bits += (t0 / 64) * lda;

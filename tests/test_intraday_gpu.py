@@ -173,3 +173,27 @@ def test_slab_default_size_unaligned_series():
         got.append((t0, t1))
 
     assert factor_panel_slabs(g, consume) == 1 and got == [(0, g.T)]
+
+
+def test_slab_split_change_rejected():
+    """The carried slab state is laid out per workgroup split ([block][split][wave]): a series
+    whose factor_split changes between slabs is rejected before any kernel runs."""
+    import torch
+    from afm import _lib
+    from afm.intraday import factor_panel_slabs, make_panel_device
+    torch.cuda.set_device(0)
+    g = make_panel_device(130, 300, seed=3)
+    ctx = _lib.Context.get()
+    before = ctx.get_option("factor_split")
+    calls = []
+
+    def consume(t0, t1, out, nanfree):
+        calls.append(t0)
+        ctx.set_option("factor_split", 5 if before != 5 else 15)
+
+    try:
+        with pytest.raises(_lib.AfmError, match="factor_split changed"):
+            factor_panel_slabs(g, consume, bars_per_slab=128)
+    finally:
+        ctx.set_option("factor_split", before)
+    assert calls == [0]
