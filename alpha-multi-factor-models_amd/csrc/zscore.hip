@@ -24,15 +24,29 @@ namespace {
 typedef unsigned long long u64;
 
 constexpr int kUnroll = 8;
+constexpr int64_t kStatsTabMax = 48 * 1024;   // reciprocal table bytes (6,143 train dates)
 
 __device__ __forceinline__ double qnan() { return __builtin_nan(""); }
 
-// grid (ceil(lda / 256), K); thread = (column k = blockIdx.y, asset a)
-__global__ __launch_bounds__(256) void zscore_stats_kernel(const double* base, int64_t col_stride,
-                                                           int64_t lda, const int32_t* cols,
-                                                           const uint64_t* bits, int64_t t0,
-                                                           int64_t t1, double* mu, double* sd) {
-    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// grid (ceil(lda / NT), K); thread = (column k = blockIdx.y, asset a).
+// TAB: the Welford quotient (val - old) / nobs by Markstein's correction from the correctly
+// rounded reciprocal RN(1 / nobs), read from an LDS table the workgroup fills first (t1 - t0 + 1
+// entries): q0 = x r, e = fma(-q0, n, x), q = fma(e, r, q0) is the IEEE quotient when nothing
+// under- or overflows (the same identity as lasso.hip div_r / analyzer.hip; a quotient outside
+// [2^-400, 2^400], a zero, an infinity or a NaN takes the IEEE division).  That is 3 f64
+// operations for the ~11 of the division sequence, with the count kept as a double (no
+// int64 -> f64 conversion per row).  1024 threads so the table is shared by 16 waves.
+template <int NT, bool TAB>
+__global__ __launch_bounds__(NT) void zscore_stats_kernel(const double* base, int64_t col_stride,
+                                                          int64_t lda, const int32_t* cols,
+                                                          const uint64_t* bits, int64_t t0,
+                                                          int64_t t1, double* mu, double* sd) {
+    extern __shared__ double rtab[];                    // [t1 - t0 + 1]: RN(1 / n), TAB only
+    if (TAB) {
+        for (int i = threadIdx.x; i <= (int)(t1 - t0); i += NT) rtab[i] = 1.0 / (double)i;
+        __syncthreads();
+    }
+    const int64_t a = (int64_t)blockIdx.x * NT + threadIdx.x;
     const int k = blockIdx.y;
     if (a >= lda) return;
     const double* x = base + (int64_t)cols[k] * col_stride + a;
@@ -40,7 +54,8 @@ __global__ __launch_bounds__(256) void zscore_stats_kernel(const double* base, i
     double sum = 0.0, comp = 0.0;
     // group_var: Welford
     double mean = 0.0, m2 = 0.0;
-    int64_t nobs = 0;
+    int nobs = 0;                                       // (dates < 2^31)
+    double dn = 0.0;                                    // nobs as a double (exact below 2^53)
     for (int64_t c = t0 >> 6; c <= (t1 - 1) >> 6; ++c) {
         u64 w = bits[c * lda + a];
         const int64_t d0 = c << 6;
@@ -65,7 +80,22 @@ __global__ __launch_bounds__(256) void zscore_stats_kernel(const double* base, i
                     if (comp != comp) comp = 0.0;
                     sum = t;
                     const double old = mean;
-                    mean = mean + (val - old) / (double)nobs;
+                    if (TAB) {
+                        dn = dn + 1.0;
+                        const double dx = val - old, r = rtab[nobs];
+                        const double q0 = dx * r;
+                        const double e = __builtin_fma(-q0, dn, dx);
+                        double q = __builtin_fma(e, r, q0);
+                        const double aq = __builtin_fabs(q0);
+                        if (!(aq > 0x1p-400 && aq < 0x1p400)) {
+                            double xd = dx;             // (volatile: the division stays behind
+                            asm volatile("" : "+v"(xd));   // the branch, not speculated)
+                            q = xd / dn;
+                        }
+                        mean = mean + q;
+                    } else {
+                        mean = mean + (val - old) / (double)nobs;
+                    }
                     m2 = m2 + (val - mean) * (val - old);
                 }
             }
@@ -140,9 +170,16 @@ extern "C" int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t co
         AFM_HIP(hipMemsetAsync(sd, 0xff, sizeof(double) * K * lda, ctx->stream));
         return AFM_OK;
     }
-    dim3 grid((unsigned)((lda + 255) / 256), (unsigned)K);
-    hipLaunchKernelGGL(zscore_stats_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride,
-                       lda, cols, bits, t0, t1, mu, sd);
+    const int64_t tab = (t1 - t0 + 1) * (int64_t)sizeof(double);
+    if (tab <= kStatsTabMax) {
+        dim3 grid((unsigned)((lda + 1023) / 1024), (unsigned)K);
+        hipLaunchKernelGGL((zscore_stats_kernel<1024, true>), grid, dim3(1024), (unsigned)tab,
+                           ctx->stream, base, col_stride, lda, cols, bits, t0, t1, mu, sd);
+    } else {
+        dim3 grid((unsigned)((lda + 255) / 256), (unsigned)K);
+        hipLaunchKernelGGL((zscore_stats_kernel<256, false>), grid, dim3(256), 0, ctx->stream,
+                           base, col_stride, lda, cols, bits, t0, t1, mu, sd);
+    }
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

@@ -1,7 +1,7 @@
 """Time afm_zscore_stats_f64 alone at config C (the pipeline's train-window statistics) and print a
-hash of mu / sd, so variants (AFM_ZS_U) can be compared for speed and bit-identity.
+hash of mu / sd, so variants (AFM_LIB=<experiment build>) can be compared for speed and bit-identity.
 
-    AFM_ZS_U=16 python tools/zs_probe.py [--assets 10000 --days 5040 --reps 5]
+    AFM_LIB=<variant .so> python tools/zs_probe.py [--assets 10000 --days 5040 --reps 5]
 """
 import argparse
 import hashlib
@@ -42,7 +42,7 @@ def main():
         torch.cuda.synchronize()
         ts.append(ev[0].elapsed_time(ev[1]))
     hsh = hashlib.sha1(pipe.mu.cpu().numpy().tobytes() + pipe.sd.cpu().numpy().tobytes()).hexdigest()
-    print(f"AFM_ZS_U={os.environ.get('AFM_ZS_U', 'default')}: zstats {np.median(ts):.3f} ms "
+    print(f"lib={os.path.basename(os.path.dirname(os.environ.get('AFM_LIB') or 'afm/default'))}: zstats {np.median(ts):.3f} ms "
           f"(min {min(ts):.3f}); mu/sd sha1 {hsh[:16]}", flush=True)
 
 
