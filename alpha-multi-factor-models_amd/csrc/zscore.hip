@@ -24,6 +24,7 @@ namespace {
 typedef unsigned long long u64;
 
 constexpr int kUnroll = 8;
+constexpr int64_t kCUs = 256;                 // MI355X compute units
 constexpr int64_t kStatsTabMax = 48 * 1024;   // reciprocal table bytes (6,143 train dates)
 
 __device__ __forceinline__ double qnan() { return __builtin_nan(""); }
@@ -35,7 +36,8 @@ __device__ __forceinline__ double qnan() { return __builtin_nan(""); }
 // under- or overflows (the same identity as lasso.hip div_r / analyzer.hip; a quotient outside
 // [2^-400, 2^400], a zero, an infinity or a NaN takes the IEEE division).  That is 3 f64
 // operations for the ~11 of the division sequence, with the count kept as a double (no
-// int64 -> f64 conversion per row).  1024 threads so the table is shared by 16 waves.
+// int64 -> f64 conversion per row).  1024 threads so the table is shared by 16 waves (256 when
+// the grid is too small to fill the chip that way).
 template <int NT, bool TAB>
 __global__ __launch_bounds__(NT) void zscore_stats_kernel(const double* base, int64_t col_stride,
                                                           int64_t lda, const int32_t* cols,
@@ -171,9 +173,16 @@ extern "C" int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t co
         return AFM_OK;
     }
     const int64_t tab = (t1 - t0 + 1) * (int64_t)sizeof(double);
-    if (tab <= kStatsTabMax) {
+    // 1,024-thread workgroups (one table per 16 waves) when they fill the chip at two per CU;
+    // a smaller grid (the per-rank shards) keeps 256-thread workgroups, so no CU sits idle
+    const int64_t wg1024 = (lda + 1023) / 1024 * K;
+    if (tab <= kStatsTabMax && wg1024 >= 2 * kCUs) {
         dim3 grid((unsigned)((lda + 1023) / 1024), (unsigned)K);
         hipLaunchKernelGGL((zscore_stats_kernel<1024, true>), grid, dim3(1024), (unsigned)tab,
+                           ctx->stream, base, col_stride, lda, cols, bits, t0, t1, mu, sd);
+    } else if (tab <= kStatsTabMax) {
+        dim3 grid((unsigned)((lda + 255) / 256), (unsigned)K);
+        hipLaunchKernelGGL((zscore_stats_kernel<256, true>), grid, dim3(256), (unsigned)tab,
                            ctx->stream, base, col_stride, lda, cols, bits, t0, t1, mu, sd);
     } else {
         dim3 grid((unsigned)((lda + 255) / 256), (unsigned)K);
