@@ -21,6 +21,17 @@ hipError_t afm_lds_opt_in(const afm_ctx* ctx, const void* kernel, int bytes) {
     return e;
 }
 
+int afm_ctx_cus(afm_ctx* ctx) {
+    if (ctx->ncu <= 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, ctx->device) !=
+                hipSuccess || n <= 0)
+            n = 256;                                            // MI355X
+        ctx->ncu = n;
+    }
+    return ctx->ncu;
+}
+
 extern "C" {
 
 const char* afm_last_error(void) { return g_last_error.c_str(); }
@@ -82,9 +93,16 @@ int afm_stream_create_cu_mask(int device, const uint32_t* cu_mask, int nwords, v
     int n = 0;
     AFM_HIP(hipGetDeviceCount(&n));
     AFM_CHECK_ARG(device >= 0 && device < n, "device ordinal out of range");
+    // the stream belongs to `device`; the calling thread's current device is restored on every
+    // exit path (torch and other callers rely on it)
+    int prev = 0;
+    AFM_HIP(hipGetDevice(&prev));
     AFM_HIP(hipSetDevice(device));
     hipStream_t s = nullptr;
-    AFM_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, cu_mask));
+    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, cu_mask);
+    const hipError_t r = hipSetDevice(prev);
+    AFM_HIP(e);
+    AFM_HIP(r);
     *out = (void*)s;
     return AFM_OK;
 }

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 
@@ -20,9 +21,17 @@ struct afm_ctx {
     int factor_fast = 1;     // clean-window fast step on
     int gram_checked = 0;    // afm_xs_gram_f64: checked staging only (no FAST + REDO passes)
     // factor slab calls: the work split each state buffer's layout was written with (the state
-    // is [block][split][wave]; a later slab under another factor_split would misread it)
+    // is [block][split][wave]; a later slab under another factor_split would misread it), and
+    // the lock guarding it (host threads may share a context)
     std::unordered_map<const void*, int> slab_types;
+    std::mutex slab_mu;
+    // compute units of the device (hipDeviceAttributeMultiprocessorCount), read once: launch
+    // shapes that fill the chip are chosen from it (0 = not read yet)
+    int ncu = 0;
 };
+
+// the context device's compute-unit count (cached in the context)
+int afm_ctx_cus(afm_ctx* ctx);
 
 void afm_set_error(const std::string& msg);
 

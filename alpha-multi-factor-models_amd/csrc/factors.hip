@@ -1654,9 +1654,7 @@ extern "C" int afm_debug_wave_cycles(long long* host, int n) {
 // at 128 VGPRs, below what the job waves need for the fast step; extra 3-way workgroups simply
 // queue for a free CU slot.
 static int factor_types(afm_ctx* ctx, int64_t nblk) {
-    int ncu = 256;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
-        ncu = 256;
+    const int ncu = afm_ctx_cus(ctx);
     int types = 3;
     for (int t : {5, 15})
         if (nblk * t <= 2 * (int64_t)ncu) types = t;
@@ -1700,11 +1698,17 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     const int64_t nwords = (t1 - t0 + 63) / 64;                   // the slab's mask words
     if (state) {                     // the state layout depends on the split: keep it per series
         const int types_now = factor_types(ctx, (A + 63) / 64);
+        std::lock_guard<std::mutex> lk(ctx->slab_mu);
         if (t0 == 0) {
             ctx->slab_types[state] = types_now;
         } else {
             const auto it = ctx->slab_types.find(state);
-            if (it != ctx->slab_types.end() && it->second != types_now) {
+            if (it == ctx->slab_types.end()) {
+                afm_set_error("factor slab: t0 > 0 continues a series whose state buffer was "
+                              "never started at t0 = 0 on this context");
+                return AFM_E_ARG;
+            }
+            if (it->second != types_now) {
                 afm_set_error("factor slab: factor_split changed between slabs of one series "
                               "(the carried state was written under another split)");
                 return AFM_E_ARG;

@@ -1654,8 +1654,10 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
         hgt[k] = 1;
     }
     __syncthreads();
-    // heights (the DAG level of an add: 1 + its children's), relaxed until they settle
-    for (int it = 0; it < kMaxLevels + 1; ++it) {
+    // heights (the DAG level of an add: 1 + its children's), relaxed until they settle: a height
+    // is at most ni, so ni + 1 rounds always settle (the loop exits at the first quiet round)
+    if (tid == 0) nlev = 0;
+    for (int it = 0; it < ni + 1; ++it) {
         bool ch = false;
         for (int k = tid; k < ni; k += 64) {
             const int a = lch[k], b = rch[k];
@@ -1666,13 +1668,24 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
         __syncthreads();
         if (__syncthreads_or(ch) == 0) break;
     }
-    if (tid <= kMaxLevels) lcount[tid] = 0;
-    if (tid == 0) nlev = 0;
+    for (int k = tid; k < ni; k += 64) atomicMax(&nlev, hgt[k]);
     __syncthreads();
-    for (int k = tid; k < ni; k += 64) {
-        atomicAdd(&lcount[hgt[k]], 1);
-        atomicMax(&nlev, hgt[k]);
+    if (nlev > kMaxLevels) {
+        // a DAG deeper than the record's level table (kMaxLevels): an error record (m = -2) the
+        // scan turns into a NaN turnover -- and so a NaN value path from this step on -- instead
+        // of writing the level counts out of bounds
+        if (tid == 0) {
+            R[0] = -2;
+            R[1] = 0;
+            R[2] = 0;
+            R[3] = 0;
+            rlen[i] = 4;
+        }
+        return;
     }
+    if (tid <= kMaxLevels) lcount[tid] = 0;
+    __syncthreads();
+    for (int k = tid; k < ni; k += 64) atomicAdd(&lcount[hgt[k]], 1);
     __syncthreads();
     const int L = nlev;
     if (tid == 0) {
@@ -1883,6 +1896,7 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                 const double size = V / 2;
                 const double qc = mdiv(size, f.s2, f.r2), qd = mdiv(size, f.s3, f.r3);
                 const double rv = 1.0 / V;                             // beside the tree
+                if (m == -2) to = __builtin_nan("");   // turnover DAG deeper than kMaxLevels
                 if (m > 0) {
                     const int* R = f.R;
                     const int nint = f.nint, L = f.L;

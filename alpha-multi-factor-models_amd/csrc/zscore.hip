@@ -24,7 +24,6 @@ namespace {
 typedef unsigned long long u64;
 
 constexpr int kUnroll = 8;
-constexpr int64_t kCUs = 256;                 // MI355X compute units
 constexpr int64_t kStatsTabMax = 48 * 1024;   // reciprocal table bytes (6,143 train dates)
 
 __device__ __forceinline__ double qnan() { return __builtin_nan(""); }
@@ -176,7 +175,7 @@ extern "C" int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t co
     // 1,024-thread workgroups (one table per 16 waves) when they fill the chip at two per CU;
     // a smaller grid (the per-rank shards) keeps 256-thread workgroups, so no CU sits idle
     const int64_t wg1024 = (lda + 1023) / 1024 * K;
-    if (tab <= kStatsTabMax && wg1024 >= 2 * kCUs) {
+    if (tab <= kStatsTabMax && wg1024 >= 2 * (int64_t)afm_ctx_cus(ctx)) {
         dim3 grid((unsigned)((lda + 1023) / 1024), (unsigned)K);
         hipLaunchKernelGGL((zscore_stats_kernel<1024, true>), grid, dim3(1024), (unsigned)tab,
                            ctx->stream, base, col_stride, lda, cols, bits, t0, t1, mu, sd);

@@ -134,7 +134,166 @@ def cpu_port(seed: int, assets: int = 150, days: int = 2520):
                       f"asset-days: " + ", ".join(f"{k} {v:.2f}s" for k, v in tm.items())}
 
 
-def variant_line(grid, cfg, steps: int, warmup: int, what: str) -> dict:
+def rooflines(pipe, stage_ms: dict, n_ad_local: int, world: int, assets: int, days: int):
+    """The factor kernel (HBM) and pooled Gram (fp64 MFMA) roofline objects of one timed
+    Pipeline, ranked by their stage's device time (dominant first)."""
+    labels_in = world == 1 and not pipe.cfg.labels_side
+    fac_bytes = FACTOR_BYTES_PER_AD if labels_in else FACTOR_BYTES_NO_LABELS
+    fac_gbs = fac_bytes * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
+    p2 = pipe.p2
+    rows_tv = float(pipe.pool_g[0, 0, 0].item())           # pooled rows (n of the Gram)
+    if pipe.sp.dup:
+        rows_tv -= float(pipe.te_gram[0, 0, 0].item())       # the duplicate is not recomputed
+    rows_tv /= (world if world > 1 else 1)
+    gram_tfs = rows_tv * p2 * (p2 + 1) / (stage_ms["xs_gram"] * 1e-3) / 1e12
+    single = world == 1
+    fac = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(fac_gbs / HBM_PEAK_GBS, 4),
+           "traffic": None,
+           "kernel": "factor_panel_kernel (+ masks, row-bit kernels%s)" % (
+               ", label planes" if labels_in else "; label planes on a side stream"),
+           "kernel_ms": round(stage_ms["factors"], 3),
+           "algorithmic_GB": round(fac_bytes * n_ad_local / 1e9, 3)}
+    tb = (pmc_traffic("factors" if labels_in else "factors_nolabels", assets, days)
+          if single else None)
+    if tb is not None:
+        fac["traffic"] = round(tb / 1e9, 3)
+        fac["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+    gram = {"bound": "mfma", "achieved": round(gram_tfs, 2), "peak": F64_MFMA_PEAK_TFS,
+            "unit": "TFLOP/s", "frac": round(gram_tfs / F64_MFMA_PEAK_TFS, 4),
+            "traffic": None, "kernel": "zgram_kernel<7,1> + tree_merge_kernel (pooled train+valid Gram)",
+            "kernel_ms": round(stage_ms["xs_gram"], 3),
+            "algorithmic_GFLOP": round(rows_tv * p2 * (p2 + 1) / 1e9, 3)}
+    tg = pmc_traffic("xs_gram", assets, days) if single else None
+    if tg is not None:
+        gram["traffic"] = round(tg / 1e9, 3)
+    ranked = sorted([(stage_ms["factors"], fac), (stage_ms["xs_gram"], gram)], key=lambda x: -x[0])
+    return [r[1] for r in ranked]
+
+
+def config_b_line(seed: int, steps: int, warmup: int) -> dict:
+    """BASELINE configs[1]: 3,000 assets x 20 years daily (5,040 days) through the same step --
+    factors -> z-score -> pooled Gram -> Lasso -> predict -> KKT rebalance -> PnL, with the
+    per-date Fama-MacBeth regressions on FM30 (~30 factors) and the analyzer's IC series on the
+    side streams, exactly the stages config B names."""
+    import torch
+    import afm
+    from afm.pipeline import PipelineConfig
+    from afm.synthetic import make_panel
+    A, T = 3000, 5040
+    grid = afm.PanelGrid.from_panel(make_panel(A, T, seed=seed, tradable_p=0.9))
+    out = variant_line(grid, PipelineConfig(), steps, warmup,
+                       f"config B (BASELINE configs[1]): {A} assets x {T} days, FM30 per-date "
+                       f"Fama-MacBeth + IC series beside the headline chain", roof=(A, T))
+    del grid
+    torch.cuda.empty_cache()
+    return out
+
+
+def config_d_line(seed: int, reps: int) -> dict:
+    """BASELINE configs[3]: 3,000 assets x 2 years of 1-minute bars (2 x 252 x 390 = 196,560
+    bars, ~5.9e8 asset-bars), the 98-column factor build by time slabs over all assets
+    (afm.intraday.factor_panel_slabs: every recurrence state and observation ring carried from
+    slab to slab; the output planes of one slab at a time fit HBM)."""
+    import torch
+    from afm.intraday import factor_panel_slabs, make_panel_device, slab_bars
+    A, T = 3000, 2 * 252 * 390
+    g = make_panel_device(A, T, seed=seed)
+    bars = int(g.valid.sum().item())
+    step = slab_bars(g)
+    n_slabs = factor_panel_slabs(g, lambda *x: None, step)           # warm-up pass
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        factor_panel_slabs(g, lambda *x: None, step)
+    ev[1].record()
+    torch.cuda.synchronize()
+    ms = ev[0].elapsed_time(ev[1]) / reps
+    byts = FACTOR_BYTES_PER_AD * bars
+    gbs = byts / (ms * 1e-3) / 1e9
+    del g
+    torch.cuda.empty_cache()
+    return {"what": f"config D (BASELINE configs[3]): {A} assets x {T} one-minute bars, 98 "
+                    f"factors by time slab ({n_slabs} slabs of {step} bars, state carried)",
+            "reps": reps, "ms_per_pass": round(ms, 2), "asset_bars": bars,
+            "value": round(bars / (ms * 1e-3), 1), "unit": "asset-bars/s",
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "factor_panel_kernel (+ masks, label planes) per slab",
+                         "algorithmic_GB": round(byts / 1e9, 1),
+                         "bytes_per_unit": FACTOR_BYTES_PER_AD}}
+
+
+def config_e_line(seed: int, reps: int, n_paths: int = 1024) -> dict:
+    """BASELINE configs[4]: bootstrap backtest -- 1,024 resampled date paths x 5,000 assets.  The
+    panel's step supplies the Lasso predictions; timed: the batched KKT rebalance of every test
+    date once (books, rolling-252 pairwise covariance, exact box-QP weights; path-independent)
+    + the 1,024 paths' turnover alignment and value recursion (KKT:842-892 per path step)."""
+    import torch
+    import afm
+    from afm.pipeline import Pipeline, PipelineConfig
+    from afm.portfolio import bootstrap_paths, bootstrap_pnl, rebalance
+    from afm.synthetic import make_panel
+    A, T = 5000, 5040
+    grid = afm.PanelGrid.from_panel(make_panel(A, T, seed=seed, tradable_p=0.9))
+    cfg = PipelineConfig()
+    pipe = Pipeline(grid, cfg)
+    pipe.step()
+    torch.cuda.synchronize()
+    paths = torch.from_numpy(bootstrap_paths(pipe.nd, n_paths, seed=2023)).cuda()
+    steps = int(paths.shape[1])
+    res = {}
+
+    def reb():
+        res["reb"] = rebalance(pipe.pred, grid.tbits, pipe.target, pipe.zrows_full, grid.close,
+                               pipe.tmr, pipe.rdates, A=A, top_n=cfg.top_n, window=cfg.window,
+                               h_range=(0, pipe.sp.tr1), lo=cfg.lo, hi=cfg.hi)
+
+    def boot():
+        res["boot"] = bootstrap_pnl(res["reb"], pipe.pred, pipe.rdates, paths, rate=cfg.rate)
+    reb()
+    boot()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    t_reb = t_boot = 0.0
+    for _ in range(reps):
+        ev[0].record()
+        reb()
+        ev[1].record()
+        boot()
+        ev[2].record()
+        torch.cuda.synchronize()
+        t_reb += ev[0].elapsed_time(ev[1])
+        t_boot += ev[1].elapsed_time(ev[2])
+    t_reb /= reps
+    t_boot /= reps
+    ok = bool(torch.isfinite(res["boot"]["value"]).all().item())
+    n_ps = n_paths * steps
+    # the per-path-step O(A) work is the id-union alignment (KKT:839): both slots' prediction
+    # presence words read (2 x lda / 8 B), plus the step's 4 PnL sums read and 4 series written
+    byts = n_ps * (2 * grid.lda // 8 + 4 * 8 + 4 * 8)
+    gbs = byts / (t_boot * 1e-3) / 1e9
+    nd = pipe.nd
+    del pipe, res
+    torch.cuda.empty_cache()
+    return {"what": f"config E (BASELINE configs[4]): {n_paths} bootstrap paths x {steps} "
+                    f"rebalance dates, {A} assets: batched KKT rebalance of the {nd} dates + the "
+                    f"paths' turnover alignment and value recursion",
+            "reps": reps, "rebalance_ms": round(t_reb, 3), "paths_ms": round(t_boot, 3),
+            "ms_per_pass": round(t_reb + t_boot, 3), "path_steps": n_ps,
+            "value": round(n_ps / ((t_reb + t_boot) * 1e-3), 1), "unit": "path-steps/s",
+            "asset_path_steps_per_s": round(A * n_ps / ((t_reb + t_boot) * 1e-3), 1),
+            "all_paths_finite": ok,
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 6), "traffic": None,
+                         "kernel": "afm_bootstrap_pnl_f64 (pred_bits + pair_union + "
+                                   "turnover_terms + pnl_scan kernels); latency-bound: one "
+                                   "sequential value recursion per path",
+                         "kernel_ms": round(t_boot, 3), "algorithmic_GB": round(byts / 1e9, 3)}}
+
+
+def variant_line(grid, cfg, steps: int, warmup: int, what: str, roof=None) -> dict:
     """Secondary timed line on the same resident panel: a PipelineConfig variant of the headline
     step, W untimed + K timed steps bracketed by synchronize, per-stage device times."""
     import numpy as np
@@ -162,6 +321,12 @@ def variant_line(grid, cfg, steps: int, warmup: int, what: str) -> dict:
            "qp_status_counts": st.tolist(), "final_value": s["final_value"]}
     w = pipe.reb["weights"][:, :, :cfg.top_n].cpu().numpy()
     out["weights_at_bounds_frac"] = round(float(((w <= cfg.lo) | (w >= cfg.hi)).mean()), 4)
+    if roof is not None:
+        out["assets"], out["days"] = roof
+        rl = rooflines(pipe, stage_ms, grid.n_asset_days(), 1, *roof)
+        out["roofline"], out["roofline_next"] = rl[0], rl[1]
+        out["fm_ms"] = stage_ms["fm"]
+        out["ic_mean"] = [round(float(x), 6) for x in s.get("ic_mean", [])]
     del pipe
     torch.cuda.empty_cache()
     return out
@@ -185,6 +350,8 @@ def main():
                          "replaced by local copies, afm.sharded.EmulatedComm): a per-rank proxy, "
                          "not a result of the job")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the config B / D / E lines (N = 1 only)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the top_n_100 / dense_lasso secondary lines (N = 1 only)")
     args = ap.parse_args()
@@ -282,42 +449,11 @@ def main():
         return
     if rank == 0:
         ms = elapsed / args.steps * 1e3
-        p2 = pipe.p2
         # roofline of the two dominant kernels, ranked by per-step device time: the factor panel
         # (HBM: 816 B per asset-day; 784 B without the two label planes, which
         # run on a side stream beside the factor kernel) and the pooled Gram (fp64 MFMA:
         # rows * (p+2)(p+3) flops over the train + valid rows, zpool + tree merges).
-        labels_in = world == 1 and not pipe.cfg.labels_side
-        fac_bytes = FACTOR_BYTES_PER_AD if labels_in else FACTOR_BYTES_NO_LABELS
-        fac_gbs = fac_bytes * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
-        rows_tv = float(pipe.pool_g[0, 0, 0].item())           # pooled rows (n of the Gram)
-        if pipe.sp.dup:
-            rows_tv -= float(pipe.te_gram[0, 0, 0].item())       # the duplicate is not recomputed
-        rows_tv /= (world if world > 1 else 1)
-        gram_tfs = rows_tv * p2 * (p2 + 1) / (stage_ms["xs_gram"] * 1e-3) / 1e12
-        single = world == 1
-        fac = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": round(fac_gbs / HBM_PEAK_GBS, 4),
-               "traffic": None,
-               "kernel": "factor_panel_kernel (+ masks, row-bit kernels%s)" % (
-                   ", label planes" if labels_in else "; label planes on a side stream"),
-               "kernel_ms": round(stage_ms["factors"], 3),
-               "algorithmic_GB": round(fac_bytes * n_ad_local / 1e9, 3)}
-        tb = (pmc_traffic("factors" if labels_in else "factors_nolabels", args.assets, args.days)
-              if single else None)
-        if tb is not None:
-            fac["traffic"] = round(tb / 1e9, 3)
-            fac["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
-        gram = {"bound": "mfma", "achieved": round(gram_tfs, 2), "peak": F64_MFMA_PEAK_TFS,
-                "unit": "TFLOP/s", "frac": round(gram_tfs / F64_MFMA_PEAK_TFS, 4),
-                "traffic": None, "kernel": "zgram_kernel<7,1> + tree_merge_kernel (pooled train+valid Gram)",
-                "kernel_ms": round(stage_ms["xs_gram"], 3),
-                "algorithmic_GFLOP": round(rows_tv * p2 * (p2 + 1) / 1e9, 3)}
-        tg = pmc_traffic("xs_gram", args.assets, args.days) if single else None
-        if tg is not None:
-            gram["traffic"] = round(tg / 1e9, 3)
-        ranked = sorted([(stage_ms["factors"], fac), (stage_ms["xs_gram"], gram)],
-                        key=lambda x: -x[0])
+        ranked = rooflines(pipe, stage_ms, n_ad_local, world, args.assets, args.days)
         res = {
             "metric": "asset-days/sec, factor build+XS regression+KKT (10k assets x 20y), "
                       "1/2/4/8 GPU",
@@ -338,8 +474,8 @@ def main():
                                        f"(solves, rebalance) x{world}") if world > 1
                        else "single"},
             "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
-            "roofline": ranked[0][1],
-            "roofline_next": ranked[1][1],
+            "roofline": ranked[0],
+            "roofline_next": ranked[1],
         }
         if world == 1 and not args.no_variants:
             # secondary lines the headline step never exercises: the active-set KKT QP on
@@ -357,6 +493,13 @@ def main():
                 grid, replace(cfg, features=DENSE_FEATURES, alpha=DENSE_ALPHA), vs, vw,
                 f"variant of KKT:433-443 / KKT:605: features without tmr_ret1d (96 columns), "
                 f"Lasso alpha {DENSE_ALPHA:g} -- a dense fit, so the predict reads its support")
+        if world == 1 and not args.no_configs:
+            # the other BASELINE configs' throughput (north_star: "throughput across the
+            # configs"), each on its own resident synthetic panel
+            cs, cw = max(2, min(args.steps, 5)), 1
+            res["config_b"] = config_b_line(args.seed, cs, cw)
+            res["config_d"] = config_d_line(args.seed, 2)
+            res["config_e"] = config_e_line(args.seed, 3)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.seed)
             res["cpu_baseline_port"] = cpu_port(args.seed)

@@ -129,11 +129,19 @@ def test_np_sum_matches_numpy_buffered_reduce():
     buffer, where the result is NOT one pairwise tree (the per-date groups and id unions of the
     10,000-asset config are ~9,000-10,000 long)."""
     from oracle.xs import np_sum
+    # The chunking is numpy's ufunc buffer size (np.getbufsize(), NPY_BUFSIZE), an implementation
+    # detail the reference does not pin: verified against numpy 2.2.6 (the goldens' version,
+    # DESIGN.md §2).  Another numpy with another buffer size fails HERE, by name, instead of the
+    # engine silently diverging from it on vectors over 8192 elements.
+    assert np.getbufsize() == 8192, (
+        f"numpy {np.__version__}: ufunc buffer size {np.getbufsize()} != 8192 -- the engine and "
+        f"oracle model numpy 2.2.6's 8192-element buffered reduction (oracle/xs_oracle.c)")
     rng = np.random.default_rng(12)
     for n in [0, 1, 7, 8, 127, 128, 129, 1000, 8191, 8192, 8193, 9000, 16384, 16385, 24577,
               40000]:
         for scale in (1.0, 1e-3, 1e8):
             v = rng.standard_normal(n) * scale * 10.0 ** rng.integers(-2, 3, n)
-            assert np_sum(v) == np.sum(v), (n, scale)
+            assert np_sum(v) == np.sum(v), (f"numpy {np.__version__}: buffered reduce differs "
+                                            f"from the 8192-chunk model", n, scale)
             sparse = np.where(rng.random(n) < 0.004, np.abs(v), 0.0)   # a turnover vector
             assert np_sum(sparse) == np.sum(sparse), (n, scale)

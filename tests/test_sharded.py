@@ -79,11 +79,12 @@ def _comm_worker(rank, world, port, outdir):
     open(os.path.join(outdir, f"ok{rank}"), "w").write("ok")
 
 
-def test_comm_gloo_collectives(tmp_path):
+@pytest.mark.parametrize("world", [2, 8])
+def test_comm_gloo_collectives(tmp_path, world):
     import torch.multiprocessing as mp
     port = _free_port()
-    mp.spawn(_comm_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
-    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+    mp.spawn(_comm_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    assert all((tmp_path / f"ok{q}").exists() for q in range(world))
 
 
 def tree_sum(v):
@@ -116,7 +117,7 @@ def _tree_worker(rank, world, port, outdir):
     open(os.path.join(outdir, f"tree{rank}"), "w").write("ok")
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_subtree_exchange_is_bit_identical(tmp_path, world):
     import torch.multiprocessing as mp
     port = _free_port()
@@ -139,7 +140,7 @@ def _paths_worker(rank, world, port, outdir):
     (Path(outdir) / f"paths{rank}").write_text("ok")
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_path_shards_gather(tmp_path, world):
     """Config E sharding: uneven path shares, one packed all-gather, rows back in path order."""
     import torch.multiprocessing as mp
@@ -195,17 +196,22 @@ def _sharded_worker(rank, world, port, outdir, A, T):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_ranks_bit_identical_to_single(tmp_path, world):
+@pytest.mark.parametrize("world,A,T", [(2, 300, 700), (4, 300, 700), (8, 1000, 640)])
+def test_sharded_ranks_bit_identical_to_single(tmp_path, world, A, T):
     """N ranks (gloo, sharing cuda:0) run the whole step: the pooled Gram, Lasso, predictions,
     FM betas, books, weights, PnL and IC are BIT-identical to the one-device step; so are the
-    config-E bootstrap paths sharded over the ranks."""
+    config-E bootstrap paths sharded over the ranks.
+
+    300 assets = 5 groups of 64: blocks of 64, ranks uneven (at N = 4 two ranks hold one group, one
+    holds a short one, one none).  World 8 -- the geometry of the 8-GPU claim:
+    1,000 assets = 16 groups, blocks of 128, so every rank owns exactly one block of the fixed
+    8-block split (rank 7 a short one of 104 assets), runs the 15-way split factor launch on its
+    shard, owns 1/8 of the FM dates (the 8-owner all_to_all) and of the rebalance dates."""
     import torch
     import torch.multiprocessing as mp
     import afm
     from afm.pipeline import Pipeline, PipelineConfig
     from afm.synthetic import make_panel
-    A, T = 300, 700                              # 5 asset groups: blocks of 64, ranks uneven
     port = _free_port()
     mp.spawn(_sharded_worker, args=(world, port, str(tmp_path), A, T), nprocs=world, join=True)
     s = np.load(tmp_path / "sharded.npz")
