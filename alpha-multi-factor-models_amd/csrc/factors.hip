@@ -34,7 +34,7 @@
 //    quotient for every integer divisor <= 64 (FMA; no contraction elsewhere); ewm skips its
 //    division by (old + alpha) == 1.0 exactly.  Other divisions are IEEE.
 //  * dropna bookkeeping: each job wave keeps its per-lane "some output NaN / non-finite at day s"
-//    bits and stores them at each 64-day word; masks_kernel ORs the kJobSets partials into
+//    bits and stores them at each 64-day word; masks_kernel ORs the partials into
 //    nanfree / finite.
 //
 // Algorithmic traffic per present asset-day: 32 B of inputs read + 98 x 8 B written = 816 B.
@@ -52,10 +52,6 @@ constexpr int kChunk = 8;
 // the loader fills chunk c+1 while the job waves scan chunk c: the ring must hold the scan's
 // lookback (57) plus two chunks
 constexpr int kRing = 57 + 2 * kChunk + 1;
-// job waves per 64-asset block (the partition W0..W14 below): three items of 5 job waves + a
-// loader, two items per workgroup = 3 waves per SIMD at <= 168 VGPRs.  (A 21-set partition at
-// 4 waves per SIMD / 128 VGPRs measured no faster: DESIGN.md §4, round 3.)
-constexpr int kJobSets = 15;
 
 typedef unsigned long long u64;
 #ifdef AFM_FP_PROFILE
@@ -83,6 +79,22 @@ struct Smem {
     double rtab[128];          // rtab[n] = 1.0 / n (IEEE), rtab[0] = +inf; indexed n & 127
     int cbyte[2][kLanes];      // presence bits of chunk c (parity c & 1), written by the loader
     int okbyte[2][kLanes];     // chunk c: 2 every present day clean (kClean), 1 warm, 0 general
+};
+// The small-grid partition (PartS below) adds, per workgroup:
+//  * rings of close.pct_change() and volume.pct_change() per observation (by observation index
+//    mod kRingR), computed ONCE by the loader -- the job waves read the returns / volume changes
+//    at any lookback instead of dividing (every return-based job: sd_*, corr_*, PVT);
+//  * the exchange of the split rolling correlations: for chunk c (parity c & 1) the numerator
+//    wave writes num, the denominator wave den, per present day; a combining wave forms
+//    num / den for chunk c during chunk c + 1 (after the barrier between them).
+// 140 KB: one workgroup per CU (the launch sizes its grid to <= the CU count).
+constexpr int kRingR = 32;           // lookbacks 0..15 + two chunks of look-ahead
+constexpr int kCorrs = 2;            // corr_5, corr_15
+struct SmemRG : Smem {
+    double r[kRingR][kLanes];
+    double g[kRingR][kLanes];
+    double xnum[kCorrs][2][kChunk][kLanes];
+    double xden[kCorrs][2][kChunk][kLanes];
 };
 
 // ---- clean windows ----------------------------------------------------------------------------
@@ -124,8 +136,12 @@ struct Args {
     const GLB double* volume;
     const GLB uint64_t* vbits;
     GLB double* out;
-    GLB uint64_t* nanpart;     // [kJobSets][words][lda] per-job-wave "some output NaN" bits
-    GLB uint64_t* badpart;     // [kJobSets][words][lda] per-job-wave "some output non-finite" bits
+    GLB uint64_t* nanpart;     // [nparts][words][lda] per-job-wave "some output NaN" bits
+    GLB uint64_t* badpart;     // [nparts][words][lda] per-job-wave "some output non-finite" bits
+    GLB uint64_t* cnanpart;    // (kernel-set) the split correlations' combiner partials
+    GLB uint64_t* cbadpart;
+    int64_t pstride;           // (kernel-set) words * lda: one partial's plane
+    int jw;                    // profiling build: job waves per item
     int types;                 // workgroups per 64-asset block (1, 3, 5 or 15)
     int fast;                  // 0: general step only (A/B tests)
     int nblk;                  // 64-asset blocks (paired launch: items = nblk * types)
@@ -201,12 +217,17 @@ constexpr ColList col_list(Cols m) {
 }
 
 // Per-lane view of one (asset, present day) step.  Lookback L reads observation p - L.
+// RG: the workgroup has the loader's return / volume-change rings (SmemRG).
+template <bool RG>
 struct Step {
+    static constexpr bool kRG = RG;
     const LDS Smem* sm;
     GLB double* out;           // output row of this day: a.out + t * lda (uniform)
     Runs* rn;
     int64_t plane;
     uint32_t voff, pmoff;      // asset * 8; (pm * kLanes + lane) * 8 (pm = p mod kRing)
+    uint32_t p32off;           // RG: ((p mod kRingR) * kLanes + lane) * 8
+    int sday, par;             // the day's index in its chunk; the chunk's parity
     uint32_t poff;             // (block * 64 + 2 * (lane & 31)) * 8: the lane's asset pair
     int64_t hmask;             // lane >= 32 ? -1 : 0
     int lane, p;
@@ -218,6 +239,16 @@ struct Step {
     }
     __device__ __forceinline__ double V(int L) const {
         return *(const LDS double*)((const LDS char*)&sm->v[0][0] + ring_off(pmoff, L));
+    }
+    // RG: return / volume change of observation p - L (NaN for observation 0), L < 16
+    __device__ __forceinline__ uint32_t rg_off(int L) const {
+        return (p32off - (uint32_t)(L * kLanes * 8)) & (uint32_t)(kRingR * kLanes * 8 - 1);
+    }
+    __device__ __forceinline__ double Rr(int L) const {
+        return *(const LDS double*)((const LDS char*)&((const LDS SmemRG*)sm)->r[0][0] + rg_off(L));
+    }
+    __device__ __forceinline__ double Gr(int L) const {
+        return *(const LDS double*)((const LDS char*)&((const LDS SmemRG*)sm)->g[0][0] + rg_off(L));
     }
     __device__ __forceinline__ double div(double x, int n) const { return div_n(sm, x, n); }
     __device__ __forceinline__ void put(int col, double x) {
@@ -268,19 +299,19 @@ struct Step {
         for (int k = 0; k + 1 < n; k += 2) store2(l.c[k], ov[l.c[k]], l.c[k + 1], ov[l.c[k + 1]]);
         if constexpr ((n & 1) != 0) store1(l.c[n - 1], ov[l.c[n - 1]]);
     }
-    // close.pct_change() at lookback L, with the window kernels' inf -> NaN (_prep_values)
+    // close.pct_change() at lookback L (p - L >= 0), NaN for observation 0
     __device__ __forceinline__ double ret(int L) const {
         if (L == 0) return r0;
+        if constexpr (RG) return Rr(L);
         const double r = C(L) / C(L + 1) - 1;
         return p - L >= 1 ? r : qnan();
     }
     __device__ __forceinline__ double volchg(int L) const {
         if (L == 0) return g0;
+        if constexpr (RG) return Gr(L);
         const double g = V(L) / V(L + 1) - 1;
         return p - L >= 1 ? g : qnan();
     }
-    __device__ __forceinline__ double fret(int L) const { return L == 0 ? r0 : C(L) / C(L + 1) - 1; }
-    __device__ __forceinline__ double fvolchg(int L) const { return L == 0 ? g0 : V(L) / V(L + 1) - 1; }
 };
 
 // A clean or warm step's view (see kClean): every ring value the wave's jobs read, gathered at the
@@ -290,14 +321,23 @@ struct Step {
 constexpr int kLook = 58;            // lookbacks 0 .. 57 (ACCEL_56 reads close 57 back)
 // s_waitcnt vmcnt(0) with expcnt / lgkmcnt left at their maxima (gfx9 encoding)
 constexpr int kWaitVm0 = 0x0f70;
-template <u64 CM, u64 VM>
-struct FastStep : Step {
-    double cc[kLook], vc[kLook];
+template <bool RG, u64 CM, u64 VM, u64 RM, u64 GM>
+struct FastStep : Step<RG> {
+    // RM / GM: the return / volume-change lookbacks the pack reads (RG: from the rings; else
+    // divided from the close / volume lookbacks L, L + 1, which CM / VM then include)
+    double cc[kLook], vc[kLook], rr[16], gg[16];
     __device__ __forceinline__ void gather() {
 #pragma unroll
         for (int L = 0; L < kLook; ++L) {
-            if ((CM >> L) & 1ull) cc[L] = C(L);
-            if ((VM >> L) & 1ull) vc[L] = V(L);
+            if ((CM >> L) & 1ull) cc[L] = this->C(L);
+            if ((VM >> L) & 1ull) vc[L] = this->V(L);
+        }
+        if constexpr (RG) {
+#pragma unroll
+            for (int L = 0; L < 16; ++L) {
+                if ((RM >> L) & 1ull) rr[L] = this->Rr(L);
+                if ((GM >> L) & 1ull) gg[L] = this->Gr(L);
+            }
         }
     }
     template <int L>
@@ -310,14 +350,19 @@ struct FastStep : Step {
         static_assert(L < kLook && ((VM >> L) & 1ull), "volume lookback not gathered");
         return vc[L];
     }
+    // return / volume change at lookback L on a clean day (every observation finite)
     template <int L>
     __device__ __forceinline__ double fret() const {
-        if constexpr (L == 0) return r0;
+        static_assert(L < 16 && ((RM >> L) & 1ull), "return lookback not declared");
+        if constexpr (L == 0) return this->r0;        // computed once per step (run_wave)
+        else if constexpr (RG) return rr[L];
         else return c<L>() / c<L + 1>() - 1;
     }
     template <int L>
     __device__ __forceinline__ double fvolchg() const {
-        if constexpr (L == 0) return g0;
+        static_assert(L < 16 && ((GM >> L) & 1ull), "volume-change lookback not declared");
+        if constexpr (L == 0) return this->g0;
+        else if constexpr (RG) return gg[L];
         else return v<L>() / v<L + 1>() - 1;
     }
 };
@@ -353,7 +398,8 @@ struct RollMean {
             neg -= __builtin_signbit(x) ? 1 : 0;
         }
     }
-    __device__ __forceinline__ double result(const Step& s, int minp, const Run& rn) const {
+    template <class S>
+    __device__ __forceinline__ double result(const S& s, int minp, const Run& rn) const {
         if (nobs >= minp && nobs > 0) {
             double r = s.div(sum, nobs);
             if (rn.same >= nobs) r = rn.prev;
@@ -410,7 +456,8 @@ struct RollVar {
         mean = ssq = cadd = crem = 0.0;
         nobs = 0;
     }
-    __device__ __forceinline__ void add(const Step& s, double x) {
+    template <class S>
+    __device__ __forceinline__ void add(const S& s, double x) {
         if (!__builtin_isnan(x)) {
             nobs = nobs + 1;
             double pm = mean - cadd, y = x - cadd, t = y - mean;
@@ -419,7 +466,8 @@ struct RollVar {
             ssq = ssq + (x - pm) * (x - mean);
         }
     }
-    __device__ __forceinline__ void remove(const Step& s, double x) {
+    template <class S>
+    __device__ __forceinline__ void remove(const S& s, double x) {
         if (!__builtin_isnan(x)) {
             nobs = nobs - 1;
             if (nobs != 0) {
@@ -433,7 +481,8 @@ struct RollVar {
             }
         }
     }
-    __device__ __forceinline__ double result(const Step& s, int minp, const Run& rn) const {
+    template <class S>
+    __device__ __forceinline__ double result(const S& s, int minp, const Run& rn) const {
         if (nobs >= minp && nobs > 1)
             return (rn.same >= nobs) ? 0.0 : s.div(ssq, nobs - 1);
         return qnan();
@@ -458,7 +507,8 @@ struct RollVar {
         return (rn.same >= W) ? 0.0 : divc<W - 1>(ssq);
     }
     // warm add: the count n = nobs after the add (1 .. W) varies per lane while the window fills
-    __device__ __forceinline__ void wadd(const Step& s, double x, int n) {
+    template <class S>
+    __device__ __forceinline__ void wadd(const S& s, double x, int n) {
         double pm = mean - cadd, y = x - cadd, t = y - mean;
         cadd = t + mean - y;
         mean = mean + s.div(t, n);
@@ -533,10 +583,11 @@ struct ComC {
 template <int W>
 struct Sma {  // No-talib.py:9-10
     static constexpr u64 kC = lb(0) | lb(W), kV = 0;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1((W - 6) / 4);
     RollMean m;
     __device__ void init() { m.init(); }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         if (s.p >= W) m.remove(s.C(W));
         m.add(s.C(0));
         s.put((W - 6) / 4, m.result(s, W, s.rn->C));
@@ -556,10 +607,11 @@ struct Sma {  // No-talib.py:9-10
 template <int W>
 struct Ema {  // No-talib.py:13-14
     static constexpr u64 kC = lb(0), kV = 0;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1(12 + (W - 6) / 4);
     Ewm e;
     __device__ void init() { e.init(); }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         s.put(12 + (W - 6) / 4, e.step(s.C(0), SpanC<W>::owf, SpanC<W>::alpha));
     }
     template <class S> __device__ void fstep(S& s) {
@@ -573,10 +625,11 @@ struct Ema {  // No-talib.py:13-14
 template <int W>
 struct Vwma {  // No-talib.py:17-19
     static constexpr u64 kC = lb(0) | lb(W), kV = lb(0) | lb(W);
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1(24 + (W - 6) / 4);
     RollMean mvc, mv;
     __device__ void init() { mvc.init(); mv.init(); }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         if (s.p >= W) {
             const double vq = s.V(W);
             mvc.remove(pinf(vq * s.C(W)));
@@ -611,11 +664,12 @@ struct Vwma {  // No-talib.py:17-19
 template <int W>
 struct Bbands {  // No-talib.py:22-26
     static constexpr u64 kC = lb(0) | lb(W), kV = 0;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1(36 + 2 * ((W - 14) / 6)) | col1(37 + 2 * ((W - 14) / 6));
     RollMean m;
     RollVar v;
     __device__ void init() { m.init(); v.init(); }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         if (s.p >= W) {
             const double xr = s.C(W);
             m.remove(xr);
@@ -657,10 +711,11 @@ struct Bbands {  // No-talib.py:22-26
 template <int W>
 struct MomAccelRocr {  // No-talib.py:35-44
     static constexpr u64 kC = lb(0) | lb(1) | lb(W) | lb(W + 1), kV = 0;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1(52 + (W - 14) / 6) | col1(60 + (W - 14) / 6) |
                                  col1(68 + (W - 14) / 6);
     __device__ void init() {}
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         const int k = (W - 14) / 6;
         double c = s.C(0);
         const double cw = s.C(W);
@@ -694,10 +749,11 @@ struct MomAccelRocr {  // No-talib.py:35-44
 template <int SLOW>
 struct Macd {  // No-talib.py:47-50
     static constexpr u64 kC = lb(0), kV = 0;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1(76 + (SLOW - 18) / 6);
     Ewm fast, slow;
     __device__ void init() { fast.init(); slow.init(); }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         double c = s.C(0);
         double f = fast.step(c, SpanC<12>::owf, SpanC<12>::alpha);
         double l = slow.step(c, SpanC<SLOW>::owf, SpanC<SLOW>::alpha);
@@ -720,10 +776,11 @@ struct Macd {  // No-talib.py:47-50
 template <int I>
 struct Rsi {  // No-talib.py:53-59
     static constexpr u64 kC = lb(0) | lb(1), kV = 0;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1(79 + (I - 8) / 6);
     Ewm up, dn;
     __device__ void init() { up.init(); dn.init(); }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         double d = s.p >= 1 ? s.C(0) - s.C(1) : qnan();
         bool nan = (d != d);
         double u = (nan || d >= 0) ? d : 0.0;          // delta.clip(lower=0)
@@ -756,15 +813,16 @@ struct Rsi {  // No-talib.py:53-59
 
 struct PvtObvPsy {  // No-talib.py:62-69
     static constexpr u64 kC = lb(0) | lb(1) | lb(14) | lb(15), kV = lb(0);
+    static constexpr u64 kRt = lb(0), kGc = 0;      // PVT's close.pct_change()
     static constexpr Cols kOut = col1(82) | col1(83) | col1(84);
     double pvt, obv;
     int ups;
     __device__ void init() { pvt = 0.0; obv = 0.0; ups = 0; }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         const int p = s.p;
         double c = s.C(0), v = s.V(0);
-        // PVT: nan-skipping cumsum of volume * pct_change
-        double term = p >= 1 ? v * (c / s.C(1) - 1) : qnan();
+        // PVT: nan-skipping cumsum of volume * pct_change (r0: NaN on observation 0)
+        double term = v * s.ret(0);
         if (term == term) pvt = pvt + term;
         s.put(82, term == term ? pvt : qnan());
         // OBV: diff <= 0 (incl. equal closes) -> -volume, else (incl. NaN diff) +volume
@@ -779,7 +837,7 @@ struct PvtObvPsy {  // No-talib.py:62-69
     }
     template <class S> __device__ void fstep(S& s) {
         const double c = FC(0), v = FV(0), c1 = FC(1);
-        pvt = pvt + v * (c / c1 - 1);
+        pvt = pvt + v * s.template fret<0>();
         s.put(82, pvt);                                   // an earlier inf term persists -> track
         obv = obv + v * ((c - c1 <= 0) ? -1.0 : 1.0);
         s.put(83, obv);
@@ -789,7 +847,7 @@ struct PvtObvPsy {  // No-talib.py:62-69
     template <class S> __device__ void wstep(S& s) {
         const int p = s.p;
         const double c = FC(0), v = FV(0), c1 = FC(1);
-        const double pv = pvt + v * (c / c1 - 1);
+        const double pv = pvt + v * s.template fret<0>();
         pvt = p >= 1 ? pv : pvt;
         s.put(82, p >= 1 ? pvt : qnan());
         obv = obv + v * ((p >= 1 && c - c1 <= 0) ? -1.0 : 1.0);   // day 0: NaN diff -> +volume
@@ -801,10 +859,10 @@ struct PvtObvPsy {  // No-talib.py:62-69
 
 template <int W, int COL>
 struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
-    static constexpr u64 kC = lb(W) | lb(W + 1), kV = 0;
+    static constexpr u64 kC = 0, kV = 0, kRt = lb(0) | lb(W), kGc = 0;
     RollVar v;
     __device__ void init() { v.init(); }
-    __device__ double step(Step& s) {
+    template <class S> __device__ double step(S& s) {
         if (s.p >= W) v.remove(s, pinf(s.ret(W)));
         v.add(s, pinf(s.ret(0)));
         double r = zsqrt(v.result(s, W, s.rn->R));
@@ -813,7 +871,7 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
     }
     template <class S> __device__ double fstep(S& s) {
         v.fremove<W>(s.template fret<W>());
-        v.fadd<W>(s.r0);
+        v.fadd<W>(s.template fret<0>());
         const double r = zsqrt(v.fresult<W>(s.rn->R));
         s.putf(COL, r);
         return r;
@@ -821,7 +879,7 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
     // returns start at p = 1: the window holds min(p, W) of them, the first remove is at W + 1
     template <class S> __device__ double wstep(S& s) {
         if (s.p >= W + 1) v.fremove<W>(s.template fret<W>());
-        if (s.p >= 1) v.wadd(s, s.r0, s.p >= W ? W : s.p);
+        if (s.p >= 1) v.wadd(s, s.template fret<0>(), s.p >= W ? W : s.p);
         const double r = s.p >= W ? zsqrt(v.fresult<W>(s.rn->R)) : qnan();
         s.putf(COL, r);
         return r;
@@ -830,10 +888,10 @@ struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
 
 struct RetSd3 {
     RetSd<3, 85> a;
-    static constexpr u64 kC = RetSd<3, 85>::kC, kV = 0;
+    static constexpr u64 kC = RetSd<3, 85>::kC, kV = 0, kRt = RetSd<3, 85>::kRt, kGc = 0;
     static constexpr Cols kOut = col1(85);
     __device__ void init() { a.init(); }
-    __device__ void step(Step& s) { a.step(s); }
+    template <class S> __device__ void step(S& s) { a.step(s); }
     template <class S> __device__ void fstep(S& s) { a.fstep(s); }
     template <class S> __device__ void wstep(S& s) { a.wstep(s); }
 };
@@ -842,9 +900,10 @@ struct RetSd5x15 {  // sd_5, sd_15, sd5_15
     RetSd<5, 86> a;
     RetSd<15, 87> b;
     static constexpr u64 kC = RetSd<5, 86>::kC | RetSd<15, 87>::kC, kV = 0;
+    static constexpr u64 kRt = RetSd<5, 86>::kRt | RetSd<15, 87>::kRt, kGc = 0;
     static constexpr Cols kOut = col1(86) | col1(87) | col1(88);
     __device__ void init() { a.init(); b.init(); }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         double x = a.step(s), y = b.step(s);
         s.put(88, x / y);
     }
@@ -861,9 +920,10 @@ struct RetSd5x15 {  // sd_5, sd_15, sd5_15
 template <int W, int COL>
 struct VolSd {  // volsd_W (No-talib.py:79-80)
     static constexpr u64 kC = 0, kV = lb(0) | lb(W);
+    static constexpr u64 kRt = 0, kGc = 0;
     RollVar v;
     __device__ void init() { v.init(); }
-    __device__ double step(Step& s) {
+    template <class S> __device__ double step(S& s) {
         if (s.p >= W) v.remove(s, pinf(s.V(W)));
         v.add(s, pinf(s.V(0)));
         double r = zsqrt(v.result(s, W, s.rn->VP));
@@ -889,9 +949,10 @@ struct VolSd {  // volsd_W (No-talib.py:79-80)
 struct VolSd3 {
     VolSd<3, 89> a;
     static constexpr u64 kC = 0, kV = VolSd<3, 89>::kV;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1(89);
     __device__ void init() { a.init(); }
-    __device__ void step(Step& s) { a.step(s); }
+    template <class S> __device__ void step(S& s) { a.step(s); }
     template <class S> __device__ void fstep(S& s) { a.fstep(s); }
     template <class S> __device__ void wstep(S& s) { a.wstep(s); }
 };
@@ -900,9 +961,10 @@ struct VolSd5x15 {
     VolSd<5, 90> a;
     VolSd<15, 91> b;
     static constexpr u64 kC = 0, kV = VolSd<5, 90>::kV | VolSd<15, 91>::kV;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut = col1(90) | col1(91) | col1(92);
     __device__ void init() { a.init(); b.init(); }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         double x = a.step(s), y = b.step(s);
         s.put(92, x / y);
     }
@@ -920,7 +982,7 @@ struct VolSd5x15 {
 // inputs).  WITH_VC also emits the vol_change column.
 template <int W, bool WITH_VC>
 struct Corr {
-    static constexpr u64 kC = lb(W) | lb(W + 1), kV = lb(W) | lb(W + 1);
+    static constexpr u64 kC = 0, kV = 0, kRt = lb(0) | lb(W), kGc = lb(0) | lb(W);
     static constexpr Cols kOut = col1(94 + (W == 15 ? 1 : 0)) | (WITH_VC ? col1(93) : Cols{0, 0});
     RollMean mxy, mx, my;
     RollVar vx, vy;
@@ -929,12 +991,13 @@ struct Corr {
         mxy.init(); mx.init(); my.init(); vx.init(); vy.init();
         cnt = 0;
     }
-    __device__ __forceinline__ static void xy(Step& s, int L, double& X, double& Y) {
+    template <class S>
+    __device__ __forceinline__ static void xy(S& s, int L, double& X, double& Y) {
         double r = s.ret(L), g = s.volchg(L);
         X = pinf(r + 0 * g);
         Y = pinf(g + 0 * r);
     }
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         double X, Y;
         if (s.p >= W) {
             xy(s, W, X, Y);
@@ -963,7 +1026,8 @@ struct Corr {
     }
     // clean: X = ret, Y = vol_change (finite), cnt = W; c / (c - 1) is the constant W / (W - 1)
     template <class S> __device__ void fstep(S& s) {
-        const double Xr = s.template fret<W>(), Yr = s.template fvolchg<W>(), X = s.r0, Y = s.g0;
+        const double Xr = s.template fret<W>(), Yr = s.template fvolchg<W>();
+        const double X = s.template fret<0>(), Y = s.template fvolchg<0>();
         const double XYr = Xr * Yr, XY = X * Y;
         mxy.fremove(XYr);
         mx.fremove(Xr);
@@ -990,7 +1054,7 @@ struct Corr {
         const bool rm = s.p >= W + 1, ad = s.p >= 1;
         const int n = s.p >= W ? W : s.p;
         const double Xr = rm ? s.template fret<W>() : 0.0, Yr = rm ? s.template fvolchg<W>() : 0.0;
-        const double X = ad ? s.r0 : 0.0, Y = ad ? s.g0 : 0.0;
+        const double X = ad ? s.template fret<0>() : 0.0, Y = ad ? s.template fvolchg<0>() : 0.0;
         const double XYr = Xr * Yr, XY = X * Y;
         mxy.wstep(XYr, XY, n);
         mx.wstep(Xr, X, n);
@@ -1011,9 +1075,151 @@ struct Corr {
         const double num = (mxy.fresult<W>(s.rn->XY) - mx.fresult<W>(s.rn->X) * my.fresult<W>(s.rn->Y)) * cf;
         const double den = __builtin_sqrt(vx.fresult<W>(s.rn->X) * vy.fresult<W>(s.rn->Y));
         s.put(94 + (W == 15 ? 1 : 0), s.p >= W ? num / den : qnan());
-        if (WITH_VC) s.putf(93, ad ? s.g0 : qnan());
+        if (WITH_VC) s.putf(93, ad ? s.template fvolchg<0>() : qnan());
     }
 };
+
+// The rolling correlation split over two waves of one workgroup (PartS, small grids: the unsplit
+// Corr is ~180 VALU per step, the longest dependency chain of the kernel).  CorrM keeps the three
+// rolling means and the count -> the numerator (mean(XY) - mean(X) mean(Y)) * c / (c - 1); CorrV
+// the two rolling variances -> the denominator sqrt(var(X) var(Y)).  Each writes its value of
+// every present day into the workgroup's exchange (SmemRG xnum / xden [K][parity][day]); the
+// wave holding Comb<K> forms num / den one chunk later (run_wave).  The same operations on the
+// same states as Corr, so the column is bit-identical.  Days before the window is full get a
+// NaN numerator (NaN / den = the NaN Corr stores there).  Needs RG (returns from the rings).
+template <int W, bool WITH_VC>
+struct CorrM {
+    static constexpr int K = W == 15 ? 1 : 0;
+    static constexpr u64 kC = 0, kV = 0, kRt = lb(0) | lb(W), kGc = lb(0) | lb(W);
+    static constexpr Cols kOut = WITH_VC ? col1(93) : Cols{0, 0};
+    RollMean mxy, mx, my;
+    int cnt;
+    __device__ void init() {
+        mxy.init(); mx.init(); my.init();
+        cnt = 0;
+    }
+    template <class S> __device__ __forceinline__ static void xput(S& s, double v) {
+        static_assert(S::kRG, "the split correlation needs the SmemRG exchange");
+        ((LDS SmemRG*)s.sm)->xnum[K][s.par][s.sday][s.lane] = v;
+    }
+    template <class S> __device__ void step(S& s) {
+        double X, Y;
+        if (s.p >= W) {
+            Corr<W, false>::xy(s, W, X, Y);
+            mxy.remove(X * Y);
+            mx.remove(X);
+            my.remove(Y);
+            double t0 = X + Y;
+            cnt -= (t0 == t0) ? 1 : 0;
+        }
+        Corr<W, false>::xy(s, 0, X, Y);
+        mxy.add(X * Y);
+        mx.add(X);
+        my.add(Y);
+        double t = X + Y;
+        cnt += (t == t) ? 1 : 0;
+        double c = (double)cnt;
+        const double cf = cnt >= 1 ? s.div(c, cnt - 1) : -c;      // c / (c - 1)
+        xput(s, (mxy.result(s, W, s.rn->XY) - mx.result(s, W, s.rn->X) * my.result(s, W, s.rn->Y)) * cf);
+        if (WITH_VC) s.put(93, s.volchg(0));
+    }
+    template <class S> __device__ void fstep(S& s) {
+        const double Xr = s.template fret<W>(), Yr = s.template fvolchg<W>();
+        const double X = s.template fret<0>(), Y = s.template fvolchg<0>();
+        const double XYr = Xr * Yr, XY = X * Y;
+        mxy.fremove(XYr);
+        mx.fremove(Xr);
+        my.fremove(Yr);
+        mxy.fadd(XY);
+        mx.fadd(X);
+        my.fadd(Y);
+        mxy.fsigns(XY, XYr);
+        mx.fsigns(X, Xr);
+        my.fsigns(Y, Yr);
+        constexpr double cf = (double)W / (double)(W - 1);
+        xput(s, (mxy.fresult<W>(s.rn->XY) - mx.fresult<W>(s.rn->X) * my.fresult<W>(s.rn->Y)) * cf);
+        if (WITH_VC) s.putf(93, Y);
+    }
+    template <class S> __device__ void wstep(S& s) {
+        const bool rm = s.p >= W + 1, ad = s.p >= 1;
+        const int n = s.p >= W ? W : s.p;
+        const double Xr = rm ? s.template fret<W>() : 0.0, Yr = rm ? s.template fvolchg<W>() : 0.0;
+        const double X = ad ? s.template fret<0>() : 0.0, Y = ad ? s.template fvolchg<0>() : 0.0;
+        const double XYr = Xr * Yr, XY = X * Y;
+        mxy.wstep(XYr, XY, n);
+        mx.wstep(Xr, X, n);
+        my.wstep(Yr, Y, n);
+        mxy.fsigns(XY, XYr);
+        mx.fsigns(X, Xr);
+        my.fsigns(Y, Yr);
+        cnt = n;
+        constexpr double cf = (double)W / (double)(W - 1);
+        const double num = (mxy.fresult<W>(s.rn->XY) - mx.fresult<W>(s.rn->X) * my.fresult<W>(s.rn->Y)) * cf;
+        xput(s, s.p >= W ? num : qnan());
+        if (WITH_VC) s.putf(93, ad ? s.template fvolchg<0>() : qnan());
+    }
+};
+
+template <int W>
+struct CorrV {
+    static constexpr int K = W == 15 ? 1 : 0;
+    static constexpr u64 kC = 0, kV = 0, kRt = lb(0) | lb(W), kGc = lb(0) | lb(W);
+    static constexpr Cols kOut{0, 0};
+    RollVar vx, vy;
+    __device__ void init() { vx.init(); vy.init(); }
+    template <class S> __device__ __forceinline__ static void xput(S& s, double v) {
+        static_assert(S::kRG, "the split correlation needs the SmemRG exchange");
+        ((LDS SmemRG*)s.sm)->xden[K][s.par][s.sday][s.lane] = v;
+    }
+    template <class S> __device__ void step(S& s) {
+        double X, Y;
+        if (s.p >= W) {
+            Corr<W, false>::xy(s, W, X, Y);
+            vx.remove(s, X);
+            vy.remove(s, Y);
+        }
+        Corr<W, false>::xy(s, 0, X, Y);
+        vx.add(s, X);
+        vy.add(s, Y);
+        xput(s, __builtin_sqrt(vx.result(s, W, s.rn->X) * vy.result(s, W, s.rn->Y)));
+    }
+    template <class S> __device__ void fstep(S& s) {
+        const double Xr = s.template fret<W>(), Yr = s.template fvolchg<W>();
+        const double X = s.template fret<0>(), Y = s.template fvolchg<0>();
+        vx.fremove<W>(Xr);
+        vy.fremove<W>(Yr);
+        vx.fadd<W>(X);
+        vy.fadd<W>(Y);
+        xput(s, __builtin_sqrt(vx.fresult<W>(s.rn->X) * vy.fresult<W>(s.rn->Y)));
+    }
+    template <class S> __device__ void wstep(S& s) {
+        const bool rm = s.p >= W + 1, ad = s.p >= 1;
+        const int n = s.p >= W ? W : s.p;
+        if (rm) {
+            vx.fremove<W>(s.template fret<W>());
+            vy.fremove<W>(s.template fvolchg<W>());
+        }
+        if (ad) {
+            vx.wadd(s, s.template fret<0>(), n);
+            vy.wadd(s, s.template fvolchg<0>(), n);
+        }
+        xput(s, __builtin_sqrt(vx.fresult<W>(s.rn->X) * vy.fresult<W>(s.rn->Y)));
+    }
+};
+
+// Marks the wave that combines split correlation K (num / den of the previous chunk, its column
+// stores and NaN bits; run_wave).  No per-day work.
+template <int K>
+struct Comb {
+    static constexpr u64 kC = 0, kV = 0, kRt = 0, kGc = 0;
+    static constexpr Cols kOut{0, 0};
+    __device__ void init() {}
+    template <class S> __device__ void step(S&) {}
+    template <class S> __device__ void fstep(S&) {}
+    template <class S> __device__ void wstep(S&) {}
+};
+template <class T> struct Comb_of { static constexpr unsigned value = 0; };
+template <int K> struct Comb_of<Comb<K>> { static constexpr unsigned value = 1u << K; };
 
 // ---- job packs ------------------------------------------------------------------------------
 // Series flags: which per-step inputs / runs a pack reads.
@@ -1029,16 +1235,19 @@ template <> struct Ser<RetSd5x15> { static constexpr unsigned value = kSerR; };
 template <> struct Ser<VolSd3> { static constexpr unsigned value = kSerVP; };
 template <> struct Ser<VolSd5x15> { static constexpr unsigned value = kSerVP; };
 template <int W, bool V> struct Ser<Corr<W, V>> { static constexpr unsigned value = kSerXY; };
+template <int W, bool V> struct Ser<CorrM<W, V>> { static constexpr unsigned value = kSerXY; };
+template <int W> struct Ser<CorrV<W>> { static constexpr unsigned value = kSerXY; };
 
 template <class... J>
 struct Pack;
 template <>
 struct Pack<> {
-    static constexpr unsigned kSer = 0;
+    static constexpr unsigned kSer = 0, kComb = 0;
     static constexpr u64 kC = 0, kV = 0;
+    static constexpr u64 kRt = 0, kGc = 0;
     static constexpr Cols kOut{0, 0};
     __device__ void init() {}
-    __device__ void step(Step&) {}
+    template <class S> __device__ void step(S&) {}
     template <class S> __device__ void fstep(S&) {}
     template <class S> __device__ void wstep(S&) {}
 };
@@ -1047,13 +1256,16 @@ struct Pack<H, R...> {
     static constexpr unsigned kSer = Ser<H>::value | Pack<R...>::kSer;
     // the lookbacks the jobs' clean / warm steps read
     static constexpr u64 kC = H::kC | Pack<R...>::kC, kV = H::kV | Pack<R...>::kV;
+    static constexpr u64 kRt = H::kRt | Pack<R...>::kRt, kGc = H::kGc | Pack<R...>::kGc;
+    // the split correlations this wave combines (bit k: corr k, see Comb)
+    static constexpr unsigned kComb = Comb_of<H>::value | Pack<R...>::kComb;
     static constexpr Cols kOut = H::kOut | Pack<R...>::kOut;
     H h;
     Pack<R...> r;
     __device__ void init() { h.init(); r.init(); }
     // the general step (cold) runs its jobs one after the other: interleaving them would raise
     // the register pressure of the whole scan
-    __device__ void step(Step& s) {
+    template <class S> __device__ void step(S& s) {
         h.step(s);
         __builtin_amdgcn_sched_barrier(0);
         r.step(s);
@@ -1069,7 +1281,8 @@ struct Pack<H, R...> {
     }
 };
 
-// Static job partition over the 15 job waves of one block: 3 item types of 5 job sets.
+// ---- partitions ----------------------------------------------------------------------------
+// PartC (large grids, config C): the 15 job sets of one block, 3 item types of 5 job sets.
 // Round 4: per type three light sets (the two rolling correlations alone, ...) at wave positions
 // 0, 2, 4 -- the SIMDs that carry three job waves of a paired workgroup -- and two heavy ones
 // (6-7 moving sums / bands) at positions 1, 3, the SIMDs the loaders share.  Config C: the same
@@ -1079,34 +1292,91 @@ struct Pack<H, R...> {
 // A variant that moved one moving sum from each heavy set to a light one ran slower at both
 // sizes (11.0 / 4.7 ms).  The heavy sets' fast steps keep <= 8 scratch accesses (slab entry
 // reloads; the day loop's chains have none).
+struct PartC {
+    static constexpr int kSets = 15;
+    static constexpr bool kRG = false;
+    template <int K> struct Set;
+};
 #ifdef AFM_FP_CENSUS_W0     // instruction census of one job alone (tools/job_census.sh)
-using W0 = Pack<AFM_FP_CENSUS_W0>;
+template <> struct PartC::Set<0> { using type = Pack<AFM_FP_CENSUS_W0>; };
 #else
-using W0 = Pack<Corr<5, true>>;
+template <> struct PartC::Set<0> { using type = Pack<Corr<5, true>>; };
 #endif
-using W1 = Pack<Bbands<32>, Vwma<30>, MomAccelRocr<32>, Ema<30>, Ema<6>, Sma<30>, Sma<18>>;
-using W2 = Pack<Bbands<14>, Vwma<14>, Ema<14>>;
-using W3 = Pack<Bbands<38>, Vwma<38>, MomAccelRocr<38>, Ema<38>, Ema<10>, Sma<38>, Sma<22>>;
-using W4 = Pack<Rsi<20>, Vwma<22>, MomAccelRocr<14>, Sma<14>, Macd<18>>;
-using W5 = Pack<Corr<15, false>>;
-using W6 = Pack<Bbands<44>, Vwma<42>, MomAccelRocr<44>, Ema<42>, Ema<22>, Sma<42>, Sma<26>>;
-using W7 = Pack<Bbands<20>, Vwma<18>, Ema<18>>;
-using W8 = Pack<Bbands<50>, Vwma<46>, MomAccelRocr<50>, Ema<46>, Ema<50>, Sma<46>, Sma<34>>;
-using W9 = Pack<RetSd5x15, VolSd3, Sma<6>>;
-using W10 = Pack<VolSd5x15, Rsi<8>>;
-using W11 = Pack<Bbands<56>, Vwma<50>, Vwma<34>, MomAccelRocr<56>, Sma<50>>;
-using W12 = Pack<PvtObvPsy, RetSd3, Rsi<14>, Sma<10>>;
-using W13 = Pack<Vwma<6>, Vwma<10>, MomAccelRocr<20>, MomAccelRocr<26>, Ema<34>, Macd<24>, Macd<30>>;
-using W14 = Pack<Bbands<26>, Vwma<26>, Ema<26>>;
-#define AFM_FP_FOR_SETS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) \
-    X(13) X(14)
+template <> struct PartC::Set<1> { using type = Pack<Bbands<32>, Vwma<30>, MomAccelRocr<32>, Ema<30>, Ema<6>, Sma<30>, Sma<18>>; };
+template <> struct PartC::Set<2> { using type = Pack<Bbands<14>, Vwma<14>, Ema<14>>; };
+template <> struct PartC::Set<3> { using type = Pack<Bbands<38>, Vwma<38>, MomAccelRocr<38>, Ema<38>, Ema<10>, Sma<38>, Sma<22>>; };
+template <> struct PartC::Set<4> { using type = Pack<Rsi<20>, Vwma<22>, MomAccelRocr<14>, Sma<14>, Macd<18>>; };
+template <> struct PartC::Set<5> { using type = Pack<Corr<15, false>>; };
+template <> struct PartC::Set<6> { using type = Pack<Bbands<44>, Vwma<42>, MomAccelRocr<44>, Ema<42>, Ema<22>, Sma<42>, Sma<26>>; };
+template <> struct PartC::Set<7> { using type = Pack<Bbands<20>, Vwma<18>, Ema<18>>; };
+template <> struct PartC::Set<8> { using type = Pack<Bbands<50>, Vwma<46>, MomAccelRocr<50>, Ema<46>, Ema<50>, Sma<46>, Sma<34>>; };
+template <> struct PartC::Set<9> { using type = Pack<RetSd5x15, VolSd3, Sma<6>>; };
+template <> struct PartC::Set<10> { using type = Pack<VolSd5x15, Rsi<8>>; };
+template <> struct PartC::Set<11> { using type = Pack<Bbands<56>, Vwma<50>, Vwma<34>, MomAccelRocr<56>, Sma<50>>; };
+template <> struct PartC::Set<12> { using type = Pack<PvtObvPsy, RetSd3, Rsi<14>, Sma<10>>; };
+template <> struct PartC::Set<13> { using type = Pack<Vwma<6>, Vwma<10>, MomAccelRocr<20>, MomAccelRocr<26>, Ema<34>, Macd<24>, Macd<30>>; };
+template <> struct PartC::Set<14> { using type = Pack<Bbands<26>, Vwma<26>, Ema<26>>; };
+
+// PartS (small grids: a multi-GPU shard, configs B / D): 30 job sets of ~1-3 recurrences each,
+// so that at a few dozen 64-asset blocks the longest per-wave dependency chain -- what bounds the
+// kernel there (a lone wave per SIMD issues its own stream, ~260 + 5 x VALU cycles
+// per day) -- is about half of PartC's.  The rolling correlations are split over two waves
+// (CorrM / CorrV), the returns and volume changes come from the loader's rings (RG), and a
+// workgroup holds J = 3, 5, 6 or 10 consecutive sets + a loader (140 KB of LDS: one per CU,
+// the grid <= the CU count).  Each correlation's two halves and its combiner (on the CorrV wave)
+// are sets 0-1 / 3-4, in one workgroup for every J.
+struct PartS {
+    static constexpr int kSets = 30;
+    static constexpr bool kRG = true;
+    template <int K> struct Set;
+};
+template <> struct PartS::Set<0> { using type = Pack<CorrM<5, true>, Ema<6>>; };
+template <> struct PartS::Set<1> { using type = Pack<CorrV<5>, Comb<0>>; };
+template <> struct PartS::Set<2> { using type = Pack<Bbands<14>, Ema<10>>; };
+template <> struct PartS::Set<3> { using type = Pack<CorrM<15, false>, Ema<14>>; };
+template <> struct PartS::Set<4> { using type = Pack<CorrV<15>, Comb<1>>; };
+template <> struct PartS::Set<5> { using type = Pack<Bbands<20>, Ema<18>>; };
+template <> struct PartS::Set<6> { using type = Pack<Bbands<26>, Sma<6>>; };
+template <> struct PartS::Set<7> { using type = Pack<Bbands<32>, Sma<10>>; };
+template <> struct PartS::Set<8> { using type = Pack<Bbands<38>, Sma<14>>; };
+template <> struct PartS::Set<9> { using type = Pack<Bbands<44>, Sma<18>>; };
+template <> struct PartS::Set<10> { using type = Pack<Bbands<50>, Sma<22>>; };
+template <> struct PartS::Set<11> { using type = Pack<Bbands<56>, Sma<26>>; };
+template <> struct PartS::Set<12> { using type = Pack<Vwma<6>, MomAccelRocr<14>>; };
+template <> struct PartS::Set<13> { using type = Pack<Vwma<10>, MomAccelRocr<20>>; };
+template <> struct PartS::Set<14> { using type = Pack<Vwma<14>, MomAccelRocr<26>>; };
+template <> struct PartS::Set<15> { using type = Pack<Vwma<18>, MomAccelRocr<32>>; };
+template <> struct PartS::Set<16> { using type = Pack<Vwma<22>, MomAccelRocr<38>>; };
+template <> struct PartS::Set<17> { using type = Pack<Vwma<26>, MomAccelRocr<44>>; };
+template <> struct PartS::Set<18> { using type = Pack<Vwma<30>, MomAccelRocr<50>>; };
+template <> struct PartS::Set<19> { using type = Pack<Vwma<34>, MomAccelRocr<56>>; };
+template <> struct PartS::Set<20> { using type = Pack<Vwma<38>, Sma<30>, Ema<30>>; };
+template <> struct PartS::Set<21> { using type = Pack<Vwma<42>, Sma<34>, Ema<34>>; };
+template <> struct PartS::Set<22> { using type = Pack<Vwma<46>, Sma<38>, Ema<38>>; };
+template <> struct PartS::Set<23> { using type = Pack<Vwma<50>, Sma<42>, Ema<42>>; };
+template <> struct PartS::Set<24> { using type = Pack<RetSd5x15, Sma<46>>; };
+template <> struct PartS::Set<25> { using type = Pack<VolSd5x15, Sma<50>>; };
+template <> struct PartS::Set<26> { using type = Pack<Rsi<8>, RetSd3, Ema<22>>; };
+template <> struct PartS::Set<27> { using type = Pack<Rsi<14>, VolSd3, Ema<26>>; };
+template <> struct PartS::Set<28> { using type = Pack<Rsi<20>, PvtObvPsy>; };
+template <> struct PartS::Set<29> { using type = Pack<Macd<18>, Macd<24>, Macd<30>, Ema<46>, Ema<50>>; };
+
+// mask partials of a partition: one per job set + one per split correlation's combiner
+template <class Part> constexpr int nparts() { return Part::kSets + (Part::kRG ? kCorrs : 0); }
 
 // The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
-// job waves (one per chunk).  It also publishes, per lane and
-// chunk, whether every present day of the chunk is clean (kClean).
+// job waves (one per chunk).  It also publishes, per lane and chunk, whether every present day of
+// the chunk is clean (kClean).  RG: it also computes each observation's close.pct_change() and
+// volume.pct_change() (the same IEEE expressions the job waves would: x / x_prev - 1, NaN for an
+// asset's first observation) into the SmemRG rings, index = observation mod kRingR.
+// State words (slab carry): the rings, pmod, run, cnt; RG: + the r / g rings, obs mod kRingR.
+template <bool RG>
+constexpr int loader_state_words() { return 2 * kRing + 3 + (RG ? 2 * kRingR + 1 : 0); }
+template <bool RG>
 __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane, int64_t block,
                                           GLB double* st) {
     LDS Smem& sm = *smp;
+    LDS SmemRG* rg = (LDS SmemRG*)smp;
     const int64_t asset = block * kLanes + lane_asset(lane);
     const int c0 = a.c0, nch = a.c1;
     double pc[kChunk], pv[kChunk];
@@ -1114,6 +1384,7 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
     int pmod = 0;                                   // observations before the staged chunk, mod kRing
     int run = 0;                                    // consecutive in-range observations (cap kClean)
     int cnt = 0;                                    // observations (capped at kClean)
+    int p32 = 0;                                    // RG: observations mod kRingR
     if (st && a.load_state) {                       // the ring and counters of the previous slab
         for (int q = 0; q < kRing; ++q) {
             sm.c[q][lane] = st[(2 * q) * kLanes + lane];
@@ -1122,6 +1393,20 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         pmod = (int)st[(2 * kRing) * kLanes + lane];
         run = (int)st[(2 * kRing + 1) * kLanes + lane];
         cnt = (int)st[(2 * kRing + 2) * kLanes + lane];
+        if constexpr (RG) {
+            for (int q = 0; q < kRingR; ++q) {
+                rg->r[q][lane] = st[(2 * kRing + 3 + 2 * q) * kLanes + lane];
+                rg->g[q][lane] = st[(2 * kRing + 4 + 2 * q) * kLanes + lane];
+            }
+            p32 = (int)st[(2 * kRing + 3 + 2 * kRingR) * kLanes + lane];
+        }
+    }
+    // RG: the previous observation's close / volume (the ring's newest entry)
+    double cprev = 0.0, vprev = 0.0;
+    if constexpr (RG) {
+        const int q = pmod == 0 ? kRing - 1 : pmod - 1;
+        cprev = sm.c[q][lane];
+        vprev = sm.v[q][lane];
     }
     auto load = [&](int ch) {
 #pragma unroll
@@ -1143,6 +1428,14 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
             if ((cb >> j) & 1ull) {
                 sm.c[q][lane] = pc[j];
                 sm.v[q][lane] = pv[j];
+                if constexpr (RG) {
+                    const double r = pc[j] / cprev - 1, g = pv[j] / vprev - 1;
+                    rg->r[p32][lane] = cnt > 0 ? r : qnan();
+                    rg->g[p32][lane] = cnt > 0 ? g : qnan();
+                    cprev = pc[j];
+                    vprev = pv[j];
+                    p32 = (p32 + 1) & (kRingR - 1);
+                }
                 q = q + 1 == kRing ? 0 : q + 1;
                 const bool good = pc[j] > kLo && pc[j] < kHi && pv[j] > kLo && pv[j] < kHi;
                 run = good ? (run < kClean ? run + 1 : kClean) : 0;
@@ -1174,6 +1467,13 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         st[(2 * kRing) * kLanes + lane] = (double)pmod;
         st[(2 * kRing + 1) * kLanes + lane] = (double)run;
         st[(2 * kRing + 2) * kLanes + lane] = (double)cnt;
+        if constexpr (RG) {
+            for (int q = 0; q < kRingR; ++q) {
+                st[(2 * kRing + 3 + 2 * q) * kLanes + lane] = rg->r[q][lane];
+                st[(2 * kRing + 4 + 2 * q) * kLanes + lane] = rg->g[q][lane];
+            }
+            st[(2 * kRing + 3 + 2 * kRingR) * kLanes + lane] = (double)p32;
+        }
     }
 }
 
@@ -1204,7 +1504,7 @@ __device__ __forceinline__ void state_io(GLB double* st, JobState<P>& js, int la
     }
 }
 
-template <class P>
+template <class P, bool RG>
 __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type, int wave, int lane,
                                       int64_t block, GLB double* stp) {
     LDS Smem& sm = *smp;
@@ -1214,10 +1514,16 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     const int c0 = a.c0, nch = a.c1;
     const int64_t w0 = ((int64_t)c0 * kChunk) >> 6;                     // the slab's first word
     constexpr unsigned S = P::kSer;
-    // clean / warm steps: the pack's lookbacks, plus close 1 back for the returns and volume 1
-    // back for vol_change
-    constexpr u64 CM = P::kC | lb(0) | ((S & (kSerR | kSerXY)) ? lb(1) : 0ull);
-    constexpr u64 VM = P::kV | lb(0) | ((S & kSerXY) ? lb(1) : 0ull);
+    // the return / volume-change lookbacks: the jobs' own, plus lookback 0 for the runs of the
+    // returns (R) and of the correlation pair (XY)
+    constexpr u64 RT = P::kRt | ((S & (kSerR | kSerXY)) ? lb(0) : 0ull);
+    constexpr u64 GC = P::kGc | ((S & kSerXY) ? lb(0) : 0ull);
+    // clean / warm steps: the pack's lookbacks; without the rings (RG) a return at lookback L is
+    // divided from close L and L + 1 (volume likewise)
+    constexpr u64 CM = P::kC | lb(0) | (RG ? 0ull : (RT | (RT << 1)));
+    constexpr u64 VM = P::kV | lb(0) | (RG ? 0ull : (GC | (GC << 1)));
+    constexpr unsigned KC = P::kComb;
+    static_assert(RG || KC == 0, "the correlation combiner needs the SmemRG exchange");
     P jobs;
     jobs.init();
     Runs rn;
@@ -1233,6 +1539,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
         pmod = js.pmod;
     }
     u64 nb = 0ull, fb = 0ull;   // this wave's NaN / non-finite bits of the current 64-day word
+    u64 cnb[kCorrs] = {0ull, 0ull}, cfb[kCorrs] = {0ull, 0ull};   // the combiner's, likewise
     lds_barrier();              // chunk 0 staged
 #ifdef AFM_FP_PROFILE
     const long long tstart = __builtin_readcyclecounter();
@@ -1240,7 +1547,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     long long twait = 0;
 #endif
 
-    FastStep<CM, VM> st;
+    FastStep<RG, CM, VM, RT, GC> st;
     st.sm = smp;
     st.rn = &rn;
     st.plane = a.plane;
@@ -1248,24 +1555,38 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     st.poff = (uint32_t)((block * kLanes + 2 * (lane & 31)) * 8);
     st.hmask = lane >= 32 ? -1 : 0;
     st.lane = lane;
+    // per present day: the ring offsets and, on the clean / warm paths, the returns from the
+    // rings (RG) or the gathered closes / volumes
+    auto at_day = [&](int p, int pm) {
+        st.p = p;
+        st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
+        if constexpr (RG) st.p32off = (uint32_t)((((p & (kRingR - 1)) * kLanes) + lane) * 8);
+    };
     // The steps of chunk ch over its present days, on one of the three paths (uniform in the wave).
     auto fast_chunk = [&](int ch, unsigned cb, unsigned& n8, unsigned& f8) {
         GLB double* row = a.out + (int64_t)ch * kChunk * a.lda;    // the chunk's first date row
         int p = pos, pm = pmod;
+        st.par = ch & 1;
 #pragma unroll 1
         for (int s = 0; s < kChunk; ++s, row += a.lda) {
             const bool pres = (cb >> s) & 1u;
             st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
             if (pres) {
-                st.p = p;
-                st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
+                at_day(p, pm);
+                st.sday = s;
                 st.anynan = false;
                 st.anybad = false;
                 st.gather();                          // every ring read of the step, then compute
                 __builtin_amdgcn_sched_barrier(0);
                 const double c0 = st.template c<0>(), v0 = st.template v<0>();
-                if constexpr ((S & (kSerR | kSerXY)) != 0) st.r0 = c0 / st.template c<1>() - 1;
-                if constexpr ((S & kSerXY) != 0) st.g0 = v0 / st.template v<1>() - 1;
+                if constexpr ((RT & 1ull) != 0) {
+                    if constexpr (RG) st.r0 = st.rr[0];
+                    else st.r0 = c0 / st.template c<1>() - 1;
+                }
+                if constexpr ((GC & 1ull) != 0) {
+                    if constexpr (RG) st.g0 = st.gg[0];
+                    else st.g0 = v0 / st.template v<1>() - 1;
+                }
                 if (S & kSerC) rn.C.fupd(c0);
                 if (S & kSerV) rn.V.fupd(v0);
                 if (S & kSerVP) rn.VP.fupd(v0);
@@ -1282,9 +1603,11 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                 ++p;
                 pm = pm + 1 == kRing ? 0 : pm + 1;
             }
-            if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
-                st.out = row;
-                st.template flush<P::kOut.lo, P::kOut.hi>();
+            if constexpr (P::kOut.lo != 0 || P::kOut.hi != 0) {
+                if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
+                    st.out = row;
+                    st.template flush<P::kOut.lo, P::kOut.hi>();
+                }
             }
         }
         pos = p;
@@ -1293,6 +1616,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     auto slow_chunk = [&](int ch, unsigned cb, bool warm, unsigned& n8, unsigned& f8) {
         GLB double* row = a.out + (int64_t)ch * kChunk * a.lda;
         int p = pos, pm = pmod;
+        st.par = ch & 1;
         if (warm) {
             // warm-up windows: every observation of the lane so far in range (the first kClean of
             // a listing); the fast cores with the counts of a filling window.  Before p = 57 the
@@ -1303,14 +1627,20 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                 const bool pres = (cb >> s) & 1u;
                 st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
                 if (pres) {
-                    st.p = p;
-                    st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
+                    at_day(p, pm);
+                    st.sday = s;
                     st.gather();
                     __builtin_amdgcn_sched_barrier(0);
                     const double c0 = st.template c<0>(), v0 = st.template v<0>();
                     // day 0: unused (no return yet)
-                    if constexpr ((S & (kSerR | kSerXY)) != 0) st.r0 = c0 / st.template c<1>() - 1;
-                    if constexpr ((S & kSerXY) != 0) st.g0 = v0 / st.template v<1>() - 1;
+                    if constexpr ((RT & 1ull) != 0) {
+                        if constexpr (RG) st.r0 = st.rr[0];
+                        else st.r0 = c0 / st.template c<1>() - 1;
+                    }
+                    if constexpr ((GC & 1ull) != 0) {
+                        if constexpr (RG) st.g0 = st.gg[0];
+                        else st.g0 = v0 / st.template v<1>() - 1;
+                    }
                     st.anynan = st.anybad = p < kClean - 1;
                     if (S & kSerC) rn.C.fupd(c0);
                     if (S & kSerV) rn.V.fupd(v0);
@@ -1330,9 +1660,11 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                     ++p;
                     pm = pm + 1 == kRing ? 0 : pm + 1;
                 }
-                if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
-                    st.out = row;
-                    st.template flush<P::kOut.lo, P::kOut.hi>();
+                if constexpr (P::kOut.lo != 0 || P::kOut.hi != 0) {
+                    if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
+                        st.out = row;
+                        st.template flush<P::kOut.lo, P::kOut.hi>();
+                    }
                 }
             }
         } else {
@@ -1341,18 +1673,26 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                 const bool pres = (cb >> s) & 1u;
                 st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
                 if (pres) {
-                    st.p = p;
-                    st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
+                    at_day(p, pm);
+                    st.sday = s;
                     st.anynan = false;
                     st.anybad = false;
                     const double c0 = st.C(0), v0 = st.V(0);
-                    if (S & (kSerR | kSerXY)) {
-                        const double r = c0 / st.C(1) - 1;
-                        st.r0 = p >= 1 ? r : qnan();
+                    if ((RT & 1ull) != 0) {
+                        if constexpr (RG) {
+                            st.r0 = st.Rr(0);                  // NaN on observation 0
+                        } else {
+                            const double r = c0 / st.C(1) - 1;
+                            st.r0 = p >= 1 ? r : qnan();
+                        }
                     }
-                    if (S & kSerXY) {
-                        const double g = v0 / st.V(1) - 1;
-                        st.g0 = p >= 1 ? g : qnan();
+                    if ((GC & 1ull) != 0) {
+                        if constexpr (RG) {
+                            st.g0 = st.Gr(0);
+                        } else {
+                            const double g = v0 / st.V(1) - 1;
+                            st.g0 = p >= 1 ? g : qnan();
+                        }
                     }
                     if (S & kSerC) rn.C.upd(c0);
                     if (S & kSerV) rn.V.upd(v0);
@@ -1371,14 +1711,66 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                     ++p;
                     pm = pm + 1 == kRing ? 0 : pm + 1;
                 }
-                if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
-                    st.out = row;
-                    st.template flush<P::kOut.lo, P::kOut.hi>();
+                if constexpr (P::kOut.lo != 0 || P::kOut.hi != 0) {
+                    if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {   // the whole wave: the day's stores
+                        st.out = row;
+                        st.template flush<P::kOut.lo, P::kOut.hi>();
+                    }
                 }
             }
         }
         pos = p;
         pmod = pm;
+    };
+    // store this wave's partial words of the word that chunk ch ends (SGPR row base + lane offset,
+    // as the output stores); slot: the mask-partial planes of this set or of a combiner
+    auto store_words = [&](int ch, GLB uint64_t* np, GLB uint64_t* bp, u64 n, u64 f) {
+        const int64_t wrow = (((int64_t)(ch * kChunk) >> 6) - w0) * a.lda;
+        typedef unsigned v2u __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, n),
+            __builtin_amdgcn_make_buffer_rsrc((void*)(np + wrow), 0, 0x7fffffff, 0x00020000),
+            (int)voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, f),
+            __builtin_amdgcn_make_buffer_rsrc((void*)(bp + wrow), 0, 0x7fffffff, 0x00020000),
+            (int)voff, 0, 0);
+    };
+    // the split correlations this wave combines: chunk ch's num / den (written by the CorrM /
+    // CorrV waves before the barrier that ended chunk ch) -> the corr column's rows of chunk ch
+    // (NaN where the lane is absent), its NaN bits into the combiner's own partial words
+    auto combine = [&](int ch, unsigned cb) {
+        if constexpr (KC != 0) {
+            const LDS SmemRG* rg = (const LDS SmemRG*)smp;
+            const int par = ch & 1, sh = (ch * kChunk) & 63;
+#pragma unroll
+            for (int k = 0; k < kCorrs; ++k) {
+                if (!((KC >> k) & 1u)) continue;
+                const int col = 94 + k;
+                GLB double* row = a.out + (int64_t)ch * kChunk * a.lda;
+                unsigned n8 = 0u, f8 = 0u;
+#pragma unroll 1
+                for (int s = 0; s < kChunk; ++s, row += a.lda) {
+                    const bool pres = (cb >> s) & 1u;
+                    double x = qnan();
+                    if (pres) {
+                        x = rg->xnum[k][par][s][lane] / rg->xden[k][par][s][lane];
+                        n8 |= (x != x) ? 1u << s : 0u;
+                        f8 |= !__builtin_isfinite(x) ? 1u << s : 0u;
+                    }
+                    if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {
+                        st.out = row;
+                        st.store1(col, x);
+                    }
+                }
+                cnb[k] |= (u64)n8 << sh;
+                cfb[k] |= (u64)f8 << sh;
+                if (sh + kChunk == 64 || ch + 1 == nch) {
+                    store_words(ch, a.cnanpart + k * a.pstride, a.cbadpart + k * a.pstride,
+                                cnb[k], cfb[k]);
+                    cnb[k] = 0ull;
+                    cfb[k] = 0ull;
+                }
+            }
+        }
     };
     // chunk ch done: its day bits into the word masks, stored at each word end (masks_kernel
     // ORs the job waves' partials); then the chunk barrier
@@ -1387,15 +1779,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
         nb |= (u64)n8 << sh;
         fb |= (u64)f8 << sh;
         if (sh + kChunk == 64 || ch + 1 == nch) {          // word end: this wave's partial words
-            // SGPR row base + lane offset, as the output stores
-            const int64_t wrow = (((int64_t)(ch * kChunk) >> 6) - w0) * a.lda;
-            typedef unsigned v2u __attribute__((ext_vector_type(2)));
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, nb),
-                __builtin_amdgcn_make_buffer_rsrc((void*)(a.nanpart + wrow), 0, 0x7fffffff,
-                                                  0x00020000), (int)voff, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, fb),
-                __builtin_amdgcn_make_buffer_rsrc((void*)(a.badpart + wrow), 0, 0x7fffffff,
-                                                  0x00020000), (int)voff, 0, 0);
+            store_words(ch, a.nanpart, a.badpart, nb, fb);
             nb = 0ull;
             fb = 0ull;
         }
@@ -1408,6 +1792,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
 #endif
     };
     int ch = c0;
+    unsigned cb_prev = 0u;                                  // the previous chunk's presence bits
     auto is_clean = [&](int c) {
         return __builtin_amdgcn_ballot_w64(sm.okbyte[c & 1][lane] != 2) == 0ull;
     };
@@ -1420,14 +1805,20 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
             // stores too, so that wait would drain them on every step
             {
                 unsigned n8 = 0u, f8 = 0u;
-                fast_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], n8, f8);
+                const unsigned cb = (unsigned)sm.cbyte[ch & 1][lane];
+                if (ch > c0) combine(ch - 1, cb_prev);
+                fast_chunk(ch, cb, n8, f8);
+                cb_prev = cb;
                 chunk_end(ch, n8, f8);
                 ++ch;
             }
             __builtin_amdgcn_s_waitcnt(kWaitVm0);
             while (ch < nch && is_clean(ch)) {              // the hot loop
                 unsigned n8 = 0u, f8 = 0u;
-                fast_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], n8, f8);
+                const unsigned cb = (unsigned)sm.cbyte[ch & 1][lane];
+                combine(ch - 1, cb_prev);
+                fast_chunk(ch, cb, n8, f8);
+                cb_prev = cb;
                 chunk_end(ch, n8, f8);
                 ++ch;
             }
@@ -1435,11 +1826,15 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
             const int okl = sm.okbyte[ch & 1][lane];
             const bool warm = __builtin_amdgcn_ballot_w64(okl == 0) == 0ull;
             unsigned n8 = 0u, f8 = 0u;
-            slow_chunk(ch, (unsigned)sm.cbyte[ch & 1][lane], warm, n8, f8);
+            const unsigned cb = (unsigned)sm.cbyte[ch & 1][lane];
+            if (ch > c0) combine(ch - 1, cb_prev);
+            slow_chunk(ch, cb, warm, n8, f8);
+            cb_prev = cb;
             chunk_end(ch, n8, f8);
             ++ch;
         }
     }
+    combine(nch - 1, cb_prev);          // the last chunk (its num / den: before the last barrier)
     if (stp) {
         JobState<P> js;
         js.jobs = jobs;
@@ -1451,7 +1846,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
 #ifdef AFM_FP_PROFILE
     if (lane == 0) {
         const long long tot = __builtin_readcyclecounter() - tstart;
-        const int jw = kJobSets / a.types;
+        const int jw = a.jw;
         const int slot = a.pslot;
         const long long tend = (long long)__builtin_amdgcn_s_memrealtime();
         g_wave_cycles[(slot * jw + wave) * 4 % (1 << 16)] = tot;
@@ -1462,38 +1857,58 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
 #endif
 }
 
-// words of one wave's slab-carry state (the largest job set's JobState, or a loader's ring)
+// words of one wave's slab-carry state (the largest job set's JobState, or a loader's rings)
 template <class P> constexpr int state_words() { return (int)((sizeof(JobState<P>) + 7) / 8); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-#define AFM_FP_STATE_WORDS(k) cmax(state_words<W##k>(),
-constexpr int kStateWords = AFM_FP_FOR_SETS(AFM_FP_STATE_WORDS) 2 * kRing + 3
-#define AFM_FP_CLOSE(k) )
-    AFM_FP_FOR_SETS(AFM_FP_CLOSE);
-#undef AFM_FP_STATE_WORDS
-#undef AFM_FP_CLOSE
+template <class Part, int K = 0>
+constexpr int part_state_words() {
+    if constexpr (K == Part::kSets) return loader_state_words<Part::kRG>();
+    else return cmax(state_words<typename Part::template Set<K>::type>(), part_state_words<Part, K + 1>());
+}
+constexpr int kStateWords = cmax(part_state_words<PartC>(), part_state_words<PartS>());
 
-// TYPES workgroups per block, each with J = 15 / TYPES job waves (job sets W[J*type + wave]) and
-// a loader wave.  PAIR: one workgroup runs TWO such items (two rings, 2 x (J + 1) waves), items
-// ordered type-major so a pair shares its job sets.  At 10k assets the 3-way split has 471 items
-// of 6 waves and 78 KB of LDS; at 168 VGPRs (3 waves / SIMD) two separate 6-wave workgroups
-// rarely co-reside on a CU (their waves land 2-2-1-1 on the SIMDs), so half of them ran in a
-// second round; paired, 236 workgroups of 12 waves (3 per SIMD, 156 KB LDS) are all resident.
-// Paired 3-way launch: job set k (0-4) or the loader (5) at wave position k of each half.  Wave
-// w of a workgroup issues on SIMD w % 4, so positions 0, 2, 4 of the two halves share SIMDs 0 and
-// 2 three to a SIMD, and positions 1, 3 share SIMDs 1 and 3 with the loaders (the partition above
-// puts the light sets at 0, 2, 4).
-// waves per SIMD a launch shape needs resident (the VGPR budget): the paired 3-way launch fills
-// the CU's four SIMDs evenly; the other splits allow 2 (256 VGPRs)
-template <int TYPES, bool PAIR>
-constexpr int waves_per_simd() {
-    constexpr int w = (kJobSets / TYPES + 1) * (PAIR ? 2 : 1);
-    return w >= 12 ? (w + 3) / 4 : 2;
+// Job set k of a partition on this wave (a uniform branch chain; every set's code is inlined)
+template <class Part, int K = 0>
+__device__ __forceinline__ void dispatch_set(int k, const Args& a, LDS Smem* sm, int wave, int lane,
+                                             int64_t block, GLB double* stp) {
+    if constexpr (K < Part::kSets) {
+#ifdef AFM_FP_ONLY   // instruction census (tools/pack_census.sh): one job set's code only
+        if (K == AFM_FP_ONLY && k == K) {
+#else
+        if (k == K) {
+#endif
+            run_wave<typename Part::template Set<K>::type, Part::kRG>(a, sm, 0, wave, lane, block, stp);
+            return;
+        }
+        dispatch_set<Part, K + 1>(k, a, sm, wave, lane, block, stp);
+    }
 }
 
-template <int TYPES, bool PAIR>
-__global__ __launch_bounds__(kLanes * (kJobSets / TYPES + 1) * (PAIR ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(waves_per_simd<TYPES, PAIR>())))
+// TYPES workgroups per block, each with J = kSets / TYPES job waves (job sets [J*type, J*type+J))
+// and a loader wave.  PAIR (PartC only): one workgroup runs TWO such items (two rings, 2 x (J + 1)
+// waves), items ordered type-major so a pair shares its job sets.  At 10k assets the 3-way split
+// has 471 items of 6 waves and 78 KB of LDS; at 168 VGPRs (3 waves / SIMD) two separate 6-wave
+// workgroups rarely co-reside on a CU (their waves land 2-2-1-1 on the SIMDs), so half of them ran
+// in a second round; paired, 236 workgroups of 12 waves (3 per SIMD, 156 KB LDS) are all resident.
+// Paired 3-way launch: job set k (0-4) or the loader (5) at wave position k of each half.  Wave
+// w of a workgroup issues on SIMD w % 4, so positions 0, 2, 4 of the two halves share SIMDs 0 and
+// 2 three to a SIMD, and positions 1, 3 share SIMDs 1 and 3 with the loaders (PartC puts the light
+// sets at 0, 2, 4).  PartS: one 140-KB workgroup per CU, J + 1 <= 11 waves.
+// waves per SIMD a launch shape needs resident (the VGPR budget)
+template <class Part, int TYPES, bool PAIR>
+constexpr int waves_per_simd() {
+    constexpr int w = (Part::kSets / TYPES + 1) * (PAIR ? 2 : 1);
+    if constexpr (Part::kRG) return (w + 3) / 4;          // one workgroup per CU
+    return w >= 12 ? (w + 3) / 4 : 2;
+}
+template <class Part>
+constexpr int smem_bytes() { return Part::kRG ? (int)sizeof(SmemRG) : (int)sizeof(Smem); }
+
+template <class Part, int TYPES, bool PAIR>
+__global__ __launch_bounds__(kLanes * (Part::kSets / TYPES + 1) * (PAIR ? 2 : 1)) __attribute__((amdgpu_waves_per_eu(waves_per_simd<Part, TYPES, PAIR>())))
 void factor_panel_kernel(Args a) {
-    constexpr int J = kJobSets / TYPES;
+    constexpr int J = Part::kSets / TYPES;
+    static_assert(!(PAIR && Part::kRG), "paired items: PartC only");
     // dynamic LDS: with a static size the compiler pads the VGPR allocation of the split
     // variants up to what it thinks the LDS occupancy allows
     extern __shared__ double sm_dyn[];
@@ -1521,26 +1936,22 @@ void factor_panel_kernel(Args a) {
     // this wave's slab-carry state slot
     GLB double* stp = a.state ? a.state + (((block * TYPES + type) * (J + 1) + wave) *
                                            (int64_t)kStateWords * kLanes) : nullptr;
-    if (wave == J) { load_wave(a, sm, lane, block, stp); return; }
-    // this type's partial-mask planes (keeps the type out of the job waves' registers)
+    if (wave == J) { load_wave<Part::kRG>(a, sm, lane, block, stp); return; }
+    // this set's partial-mask planes (keeps the type out of the job waves' registers); the
+    // combiners' planes follow the kSets sets'
     Args at = a;
     const int64_t w0 = ((int64_t)a.c0 * kChunk) >> 6;
-    const int64_t po = (int64_t)(type * J + wave) * ((a.t1 + 63) / 64 - w0) * a.lda;
+    at.pstride = ((a.t1 + 63) / 64 - w0) * a.lda;
+    const int64_t po = (int64_t)(type * J + wave) * at.pstride;
     at.nanpart = a.nanpart + po;
     at.badpart = a.badpart + po;
+    at.cnanpart = a.nanpart + (int64_t)Part::kSets * at.pstride;
+    at.cbadpart = a.badpart + (int64_t)Part::kSets * at.pstride;
 #ifdef AFM_FP_PROFILE
     at.pslot = (int)(block * TYPES + type);          // profile slot of this item
+    at.jw = J;
 #endif
-    switch (type * J + wave) {
-#ifdef AFM_FP_ONLY   // instruction census (tools/pack_census.sh): one job set's code only
-#define AFM_FP_CASE(k) case k: if (k == AFM_FP_ONLY) run_wave<W##k>(at, sm, 0, wave, lane, block, stp); break;
-#else
-#define AFM_FP_CASE(k) case k: run_wave<W##k>(at, sm, 0, wave, lane, block, stp); break;
-#endif
-        AFM_FP_FOR_SETS(AFM_FP_CASE)
-#undef AFM_FP_CASE
-        default: break;
-    }
+    dispatch_set<Part>(type * J + wave, at, sm, wave, lane, block, stp);
 }
 
 // nanfree = present & no type flagged a NaN; finite = present & no type flagged a non-finite
@@ -1648,42 +2059,57 @@ extern "C" int afm_debug_wave_cycles(long long* host, int n) {
 }
 #endif
 
-// workgroups per block: the most job-set splits whose workgroups are all resident at once.
-// A CU holds two 78-KB rings; the split variants (6, 4 or 2 waves) fit two workgroups per CU,
-// the unsplit one (16 waves) only one.  3 at least: the unsplit 16-wave workgroup caps the waves
-// at 128 VGPRs, below what the job waves need for the fast step; extra 3-way workgroups simply
-// queue for a free CU slot.
+// The launch shape: a partition and its workgroups per block (TYPES), as one code -- PartC:
+// 1, 3, 5 or 15; PartS: 100 + TYPES with TYPES = 10, 6, 5 or 3 (J = 3, 5, 6, 10 job waves per
+// workgroup).  (The option factor_split takes the same codes.)
+//  * PartS while its 140-KB workgroups (one per CU) all fit the device at once: the fewest job
+//    waves per workgroup that do, so a small grid keeps one wave per SIMD (its per-wave chains
+//    bound it) -- the N = 8 shard (20 blocks) J = 3, configs B / D (47 blocks) J = 6, the
+//    N = 2 shard (79 blocks) J = 10.
+//  * PartC otherwise (config C, 157 blocks): the most job-set splits whose 78-KB workgroups are
+//    all resident, two per CU; 3 at least (the unsplit 16-wave workgroup caps the waves at 128
+//    VGPRs, below what the job waves need for the fast step); extra 3-way workgroups queue.
 static int factor_types(afm_ctx* ctx, int64_t nblk) {
-    const int ncu = afm_ctx_cus(ctx);
+    if (ctx->factor_split) return ctx->factor_split;               // option factor_split
+    const int64_t ncu = afm_ctx_cus(ctx);
+    for (int t : {10, 6, 5, 3})
+        if (nblk * t <= ncu) return 100 + t;
     int types = 3;
     for (int t : {5, 15})
-        if (nblk * t <= 2 * (int64_t)ncu) types = t;
-    if (ctx->factor_split) types = ctx->factor_split;              // option factor_split
+        if (nblk * t <= 2 * ncu) types = t;
     return types;
 }
 
-// a split of the kJobSets job waves over TYPES workgroups per block: J job waves + a loader
+// a launch code is a split of its partition's job sets: J job waves + a loader per workgroup
+template <class Part>
 static constexpr bool split_ok(int types) {
-    return types >= 1 && afm::kJobSets % types == 0 && afm::kJobSets / types + 1 <= 16;
+    return types >= 1 && Part::kSets % types == 0 && Part::kSets / types + 1 <= 16 &&
+           (!Part::kRG || Part::kSets / types + 1 <= 11);
 }
-template <int TYPES, bool PAIR>
+template <class Part, int TYPES, bool PAIR>
 static int launch_split(afm_ctx* ctx, int64_t nblk, const afm::Args& a) {
-    if constexpr (!split_ok(TYPES)) {
+    if constexpr (!split_ok<Part>(TYPES)) {
         (void)ctx; (void)nblk; (void)a;
         afm_set_error("factor kernel: factor_split is not a split of the job sets");
         return AFM_E_ARG;
     } else {
-        constexpr int J = afm::kJobSets / TYPES;
-        const int bytes = (int)sizeof(afm::Smem) * (PAIR ? 2 : 1);    // > 64 KB: opt in
-        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<TYPES, PAIR>, bytes));
+        constexpr int J = Part::kSets / TYPES;
+        const int bytes = afm::smem_bytes<Part>() * (PAIR ? 2 : 1);    // > 64 KB: opt in
+        AFM_HIP(afm_lds_opt_in(ctx, (const void*)afm::factor_panel_kernel<Part, TYPES, PAIR>, bytes));
         const int64_t items = nblk * TYPES;
         const dim3 grid((unsigned)(PAIR ? (items + 1) / 2 : items));
-        hipLaunchKernelGGL((afm::factor_panel_kernel<TYPES, PAIR>), grid,
+        hipLaunchKernelGGL((afm::factor_panel_kernel<Part, TYPES, PAIR>), grid,
                            dim3(64 * (J + 1) * (PAIR ? 2 : 1)), bytes, ctx->stream, a);
         AFM_HIP(hipGetLastError());
         return AFM_OK;
     }
 }
+// mask partials of a launch code
+static int code_parts(int code) {
+    return code > 100 ? afm::nparts<afm::PartS>() : afm::nparts<afm::PartC>();
+}
+static int code_types(int code) { return code > 100 ? code - 100 : code; }
+static int code_sets(int code) { return code > 100 ? afm::PartS::kSets : afm::PartC::kSets; }
 
 // The factor kernel over the time slab [t0, t1) of the [T]-date series (t0 a multiple of 64;
 // [0, T) = the whole series).  out / nanfree / finite hold the slab's dates only.  state: the
@@ -1720,9 +2146,10 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
         if (finite_bits) finite_bits += (t0 / 64) * lda;
     }
     const int64_t nblk = (A + 63) / 64;
-    const int types = factor_types(ctx, nblk);
+    const int code = factor_types(ctx, nblk);
+    const int types = code_types(code), nparts = code_parts(code);
     uint64_t* part = nullptr;         // per-job-wave mask partials (masks_kernel ORs them)
-    AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * afm::kJobSets * nwords * lda,
+    AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * nparts * nwords * lda,
                            ctx->stream));
     afm::Args a;
     a.T = T;
@@ -1733,7 +2160,10 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     a.vbits = (const GLB uint64_t*)valid_bits;
     a.out = (GLB double*)(full ? out : out - t0 * lda);   // date t's row at a.out + t * lda
     a.nanpart = (GLB uint64_t*)part;
-    a.badpart = (GLB uint64_t*)(part + afm::kJobSets * nwords * lda);
+    a.badpart = (GLB uint64_t*)(part + nparts * nwords * lda);
+    a.cnanpart = a.cbadpart = nullptr;
+    a.pstride = 0;
+    a.jw = 0;
     a.types = types;
     a.nblk = (int)nblk;
     a.pslot = 0;
@@ -1748,12 +2178,19 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     const bool pair = ctx->factor_pair != 0;
     a.fast = ctx->factor_fast ? 1 : 0;
     int rc;
-    switch (types) {                 // paired 2-item workgroups for the 3-way split (see the kernel)
-        case 1: rc = launch_split<1, false>(ctx, nblk, a); break;
-        case 3: rc = pair ? launch_split<3, true>(ctx, nblk, a) : launch_split<3, false>(ctx, nblk, a);
+    using afm::PartC;
+    using afm::PartS;
+    switch (code) {                  // paired 2-item workgroups for the 3-way split (see the kernel)
+        case 1: rc = launch_split<PartC, 1, false>(ctx, nblk, a); break;
+        case 3: rc = pair ? launch_split<PartC, 3, true>(ctx, nblk, a)
+                          : launch_split<PartC, 3, false>(ctx, nblk, a);
                 break;
-        case 5: rc = launch_split<5, false>(ctx, nblk, a); break;
-        case 15: rc = launch_split<15, false>(ctx, nblk, a); break;
+        case 5: rc = launch_split<PartC, 5, false>(ctx, nblk, a); break;
+        case 15: rc = launch_split<PartC, 15, false>(ctx, nblk, a); break;
+        case 103: rc = launch_split<PartS, 3, false>(ctx, nblk, a); break;
+        case 105: rc = launch_split<PartS, 5, false>(ctx, nblk, a); break;
+        case 106: rc = launch_split<PartS, 6, false>(ctx, nblk, a); break;
+        case 110: rc = launch_split<PartS, 10, false>(ctx, nblk, a); break;
         default:
             afm_set_error("factor kernel: factor_split is not a split of the job sets");
             rc = AFM_E_ARG;
@@ -1767,8 +2204,8 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     // columns past A (lda padding) carry no presence: their mask words come from valid_bits
     // (zero there), and the factor kernel never ran on blocks past ceil(A/64)
     hipLaunchKernelGGL(afm::masks_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0,
-                       ctx->stream, nwords, lda, afm::kJobSets, valid_bits + (t0 / 64) * lda, part,
-                       part + afm::kJobSets * nw, nanfree_bits, finite_bits);
+                       ctx->stream, nwords, lda, nparts, valid_bits + (t0 / 64) * lda, part,
+                       part + nparts * nw, nanfree_bits, finite_bits);
     AFM_HIP(hipGetLastError());
     if (excess) {                  // NULL: the caller runs afm_labels_f64 (e.g. on another stream)
         dim3 g2((unsigned)((lda + 255) / 256), (unsigned)((t1 - 1) / 64 - t0 / 64 + 1));
@@ -1799,8 +2236,9 @@ extern "C" int afm_factors_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
 extern "C" int64_t afm_factors_state_bytes(afm_ctx* ctx, int64_t A) {
     if (!ctx || A <= 0) return -1;
     const int64_t nblk = (A + 63) / 64;
-    const int types = factor_types(ctx, nblk);
-    return nblk * types * (afm::kJobSets / types + 1) * (int64_t)afm::kStateWords * 64 * 8;
+    const int code = factor_types(ctx, nblk);
+    const int types = code_types(code);
+    return nblk * types * (code_sets(code) / types + 1) * (int64_t)afm::kStateWords * 64 * 8;
 }
 
 extern "C" int afm_factors_slab_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,

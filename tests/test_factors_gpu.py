@@ -58,12 +58,16 @@ def test_factor_grid_vs_oracle(A, T, seed, kw):
 
 
 @pytest.mark.parametrize("types,pair,A", [("1", "1", 200), ("3", "1", 200), ("3", "1", 300),
-                                          ("3", "0", 200), ("5", "1", 200), ("15", "1", 200)])
+                                          ("3", "0", 200), ("5", "1", 200), ("15", "1", 200),
+                                          ("110", "0", 200), ("106", "0", 300), ("105", "0", 200),
+                                          ("103", "0", 300)])
 def test_factor_workgroup_splits_identical(types, pair, A, monkeypatch):
-    """Every split of a block's 15 job waves over 1, 3, 5 or 15 workgroups (chosen from the
-    shard's block count; the context option factor_split overrides), paired two items per
-    workgroup or not (factor_pair; A = 300 leaves the last pair half idle), gives the same
-    bit-exact panel and masks."""
+    """Every launch shape gives the same bit-exact panel and masks: the 15-set partition split
+    over 1, 3, 5 or 15 workgroups per block (paired two items per workgroup or not, factor_pair;
+    A = 300 leaves the last pair half idle), and the 30-set small-grid partition (split
+    correlations, return rings) over 10, 6, 5 or 3 workgroups per block (codes 110 / 106 / 105 /
+    103: 3, 5, 6, 10 job waves each).  The shape is chosen from the shard's block count; the
+    context option factor_split overrides."""
     import torch
     import afm
     from afm.synthetic import make_panel
@@ -99,11 +103,13 @@ def test_factor_kernel_rejects_bad_shapes():
     torch.cuda.synchronize()
 
 
-def test_clean_fast_step_matches_general_step(monkeypatch):
+@pytest.mark.parametrize("split", [0, 3])
+def test_clean_fast_step_matches_general_step(monkeypatch, split):
     """The clean-window fast step (factors.hip kClean) and the general step give the same
     bit-exact panel, with same-value runs, zero volumes and NaN closes planted inside otherwise
     clean stretches (each forces the general step for ~58 observations, then the fast step
-    resumes on the carried states)."""
+    resumes on the carried states) -- in the small-grid partition (auto at 256 assets) and the
+    15-set one (split 3)."""
     import torch
     import afm
     from afm.synthetic import make_panel
@@ -121,7 +127,7 @@ def test_clean_fast_step_matches_general_step(monkeypatch):
     from afm import _lib
     for flag in ("1", "0"):
         fin = torch.zeros_like(grid.vbits)
-        with _lib.options(factor_fast=int(flag == "0")):
+        with _lib.options(factor_fast=int(flag == "0"), factor_split=split):
             out, nanfree = afm.factor_panel(grid, finite=fin)
         torch.cuda.synchronize()
         outs[flag] = (out.clone(), nanfree.clone(), fin.clone())

@@ -75,12 +75,14 @@ def test_group_sizing():
     assert b <= 21 and ((47 + b - 1) // b) == 3 and b == 16            # 16, 16, 15
 
 
-@pytest.mark.parametrize("types,step", [(15, 64), (5, 320), (3, 1024), (3, 704)])
+@pytest.mark.parametrize("types,step", [(15, 64), (5, 320), (3, 1024), (3, 704), (110, 64),
+                                        (106, 320), (103, 704)])
 def test_time_slabs_identical_to_one_launch(monkeypatch, types, step):
     """Config D's default build: ALL assets over consecutive time slabs, every recurrence state
     and observation ring carried across slab boundaries in the state buffer -- the concatenated
     slabs (98 planes incl. the labels, nanfree bits) equal one launch bit for bit, for every
-    workgroup split of the job sets (3 = the paired 12-wave launch)."""
+    workgroup split of the job sets (3 = the paired 12-wave launch; 1xx = the small-grid
+    partition, whose loaders also carry the return / volume-change rings)."""
     import torch
     import afm
     from afm.intraday import factor_panel_slabs, make_panel_device

@@ -24,8 +24,17 @@ def main():
     torch.cuda.synchronize()
     L = _lib.lib()
     nblk = (A + 63) // 64
-    types = int(os.environ.get('AFM_FP_TYPES', '3'))
-    jw = 15 // types
+    # AFM_FP_TYPES: the launch code the run used (factor_split; 1xx = the 30-set partition with
+    # xx workgroups per block)
+    code = int(os.environ.get('AFM_FP_TYPES', '3'))
+    if code > 100:
+        types, jw = code - 100, 30 // (code - 100)
+    else:
+        types, jw = code, 15 // code
+    if code:
+        _lib.Context.get().set_option("factor_split", code)
+        afm.factor_panel(grid)
+        torch.cuda.synchronize()
     n = nblk * types * jw * 4
     buf = (ctypes.c_longlong * n)()
     assert L.afm_debug_wave_cycles(buf, n) == 0
