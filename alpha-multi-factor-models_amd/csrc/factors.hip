@@ -1354,12 +1354,12 @@ template <> struct PartS::Set<20> { using type = Pack<Vwma<38>, Sma<30>, Ema<30>
 template <> struct PartS::Set<21> { using type = Pack<Vwma<42>, Sma<34>, Ema<34>>; };
 template <> struct PartS::Set<22> { using type = Pack<Vwma<46>, Sma<38>, Ema<38>>; };
 template <> struct PartS::Set<23> { using type = Pack<Vwma<50>, Sma<42>, Ema<42>>; };
-template <> struct PartS::Set<24> { using type = Pack<RetSd5x15, Sma<46>>; };
-template <> struct PartS::Set<25> { using type = Pack<VolSd5x15, Sma<50>>; };
+template <> struct PartS::Set<24> { using type = Pack<RetSd5x15>; };
+template <> struct PartS::Set<25> { using type = Pack<VolSd5x15>; };
 template <> struct PartS::Set<26> { using type = Pack<Rsi<8>, RetSd3, Ema<22>>; };
 template <> struct PartS::Set<27> { using type = Pack<Rsi<14>, VolSd3, Ema<26>>; };
 template <> struct PartS::Set<28> { using type = Pack<Rsi<20>, PvtObvPsy>; };
-template <> struct PartS::Set<29> { using type = Pack<Macd<18>, Macd<24>, Macd<30>, Ema<46>, Ema<50>>; };
+template <> struct PartS::Set<29> { using type = Pack<Macd<18>, Macd<24>, Macd<30>, Ema<46>, Ema<50>, Sma<46>, Sma<50>>; };
 
 // mask partials of a partition: one per job set + one per split correlation's combiner
 template <class Part> constexpr int nparts() { return Part::kSets + (Part::kRG ? kCorrs : 0); }
@@ -1555,14 +1555,47 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
     st.poff = (uint32_t)((block * kLanes + 2 * (lane & 31)) * 8);
     st.hmask = lane >= 32 ? -1 : 0;
     st.lane = lane;
-    // per present day: the ring offsets and, on the clean / warm paths, the returns from the
-    // rings (RG) or the gathered closes / volumes
-    auto at_day = [&](int p, int pm) {
-        st.p = p;
-        st.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
-        if constexpr (RG) st.p32off = (uint32_t)((((p & (kRingR - 1)) * kLanes) + lane) * 8);
+    using FS = FastStep<RG, CM, VM, RT, GC>;
+    // one clean day of step object x (its ring offsets set): gather, the per-day values and
+    // runs, the jobs' fast steps, the day's NaN bits
+    auto fast_day = [&](FS& x, int s, unsigned& n8, unsigned& f8) {
+        x.sday = s;
+        x.anynan = false;
+        x.anybad = false;
+        const double c0 = x.template c<0>(), v0 = x.template v<0>();
+        if constexpr ((RT & 1ull) != 0) {
+            if constexpr (RG) x.r0 = x.rr[0];
+            else x.r0 = c0 / x.template c<1>() - 1;
+        }
+        if constexpr ((GC & 1ull) != 0) {
+            if constexpr (RG) x.g0 = x.gg[0];
+            else x.g0 = v0 / x.template v<1>() - 1;
+        }
+        if (S & kSerC) rn.C.fupd(c0);
+        if (S & kSerV) rn.V.fupd(v0);
+        if (S & kSerVP) rn.VP.fupd(v0);
+        if (S & kSerVC) rn.VC.fupd(v0 * c0);
+        if (S & kSerR) rn.R.fupd(x.r0);
+        if (S & kSerXY) {
+            rn.X.fupd(x.r0);
+            rn.Y.fupd(x.g0);
+            rn.XY.fupd(x.r0 * x.g0);
+        }
+        jobs.fstep(x);
+        n8 |= x.anynan ? 1u << s : 0u;
+        f8 |= x.anybad ? 1u << s : 0u;
+    };
+    // per present day: the ring offsets of observation p (pm = p mod kRing)
+    auto set_day = [&](FS& x, int p, int pm) {
+        x.p = p;
+        x.pmoff = (uint32_t)((pm * kLanes + lane) * 8);
+        if constexpr (RG) x.p32off = (uint32_t)((((p & (kRingR - 1)) * kLanes) + lane) * 8);
     };
     // The steps of chunk ch over its present days, on one of the three paths (uniform in the wave).
+    // (Round 5 measured two consecutive days with the same present lanes fused into one
+    // straight-line step -- both days' ring reads in one batch: slower, 2.76 vs 2.54 ms at 1,250
+    // assets, 4.2 vs 3.9 at 3,000; the scheduler kept day s's output chain ahead of day s + 1's
+    // updates and the pair test cost more than it overlapped.  DESIGN.md §4.)
     auto fast_chunk = [&](int ch, unsigned cb, unsigned& n8, unsigned& f8) {
         GLB double* row = a.out + (int64_t)ch * kChunk * a.lda;    // the chunk's first date row
         int p = pos, pm = pmod;
@@ -1572,34 +1605,10 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
             const bool pres = (cb >> s) & 1u;
             st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
             if (pres) {
-                at_day(p, pm);
-                st.sday = s;
-                st.anynan = false;
-                st.anybad = false;
+                set_day(st, p, pm);
                 st.gather();                          // every ring read of the step, then compute
                 __builtin_amdgcn_sched_barrier(0);
-                const double c0 = st.template c<0>(), v0 = st.template v<0>();
-                if constexpr ((RT & 1ull) != 0) {
-                    if constexpr (RG) st.r0 = st.rr[0];
-                    else st.r0 = c0 / st.template c<1>() - 1;
-                }
-                if constexpr ((GC & 1ull) != 0) {
-                    if constexpr (RG) st.g0 = st.gg[0];
-                    else st.g0 = v0 / st.template v<1>() - 1;
-                }
-                if (S & kSerC) rn.C.fupd(c0);
-                if (S & kSerV) rn.V.fupd(v0);
-                if (S & kSerVP) rn.VP.fupd(v0);
-                if (S & kSerVC) rn.VC.fupd(v0 * c0);
-                if (S & kSerR) rn.R.fupd(st.r0);
-                if (S & kSerXY) {
-                    rn.X.fupd(st.r0);
-                    rn.Y.fupd(st.g0);
-                    rn.XY.fupd(st.r0 * st.g0);
-                }
-                jobs.fstep(st);
-                n8 |= st.anynan ? 1u << s : 0u;
-                f8 |= st.anybad ? 1u << s : 0u;
+                fast_day(st, s, n8, f8);
                 ++p;
                 pm = pm + 1 == kRing ? 0 : pm + 1;
             }
@@ -1627,7 +1636,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                 const bool pres = (cb >> s) & 1u;
                 st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
                 if (pres) {
-                    at_day(p, pm);
+                    set_day(st, p, pm);
                     st.sday = s;
                     st.gather();
                     __builtin_amdgcn_sched_barrier(0);
@@ -1673,7 +1682,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
                 const bool pres = (cb >> s) & 1u;
                 st.template reset<P::kOut.lo, P::kOut.hi>();   // absent lanes store NaN
                 if (pres) {
-                    at_day(p, pm);
+                    set_day(st, p, pm);
                     st.sday = s;
                     st.anynan = false;
                     st.anybad = false;
