@@ -5,7 +5,7 @@ set -o pipefail
 TAG=$1; R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_prof -o run --output-format csv -- \
-    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-variants > $R/gpurun_out/${TAG}_prof.log 2>&1 \
+    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-variants --no-configs > $R/gpurun_out/${TAG}_prof.log 2>&1 \
     || { echo "prof failed"; tail -20 $R/gpurun_out/${TAG}_prof.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/${TAG}_prof8 -o run --output-format csv -- \
     python3 $R/bench.py --steps 5 --warmup 2 --emulate-world 8 > $R/gpurun_out/${TAG}_prof8.log 2>&1 \
