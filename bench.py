@@ -352,6 +352,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the config B / D / E lines (N = 1 only)")
+    ap.add_argument("--config-only", choices=("b", "d", "e"), default=None,
+                    help="run only that config line and print it (profiling runs)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the top_n_100 / dense_lasso secondary lines (N = 1 only)")
     args = ap.parse_args()
@@ -363,6 +365,13 @@ def main():
     import afm
     from afm.pipeline import PIPELINE_STAGES, Pipeline, PipelineConfig
     from afm.synthetic import make_panel
+
+    if args.config_only:
+        fn = {"b": lambda: config_b_line(args.seed, max(2, min(args.steps, 5)), 1),
+              "d": lambda: config_d_line(args.seed, 2),
+              "e": lambda: config_e_line(args.seed, 3)}[args.config_only]
+        print(json.dumps({"config_" + args.config_only: fn()}), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
