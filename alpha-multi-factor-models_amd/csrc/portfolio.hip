@@ -23,6 +23,7 @@
 //   -> 0 included, evaluated sparsely at the members' union positions).
 #include "afm_internal.h"
 
+#include <algorithm>
 #include <type_traits>
 #include <vector>
 
@@ -1565,19 +1566,29 @@ __device__ int pw_lca_depth(int64_t n, int64_t p, int64_t q) {
 // Steps i are grouped in sequences of `seq` (one bootstrap path each; seq = nd for the plain
 // rebalance sequence); the book of step i is book slot ix(i) (idx = nullptr: slot i).  upos /
 // usize are per step.
+// Two kernels build the records (round 5): turnover_terms_wave_kernel, one wave per step with
+// every stage in registers, for steps whose books (this step's and the previous one's) hold at
+// most kWaveK names -- the headline's top_n = 10 and every bootstrap path step of config E -- and
+// turnover_terms_kernel below, a persistent grid over the remaining steps (larger books: LDS
+// arrays of kMaxTerms).  The records differ only in the order of the adds inside a DAG level
+// (any order within a level evaluates the same additions), so the turnover is bitwise the same.
+constexpr int kWaveK = 16;                   // 2 books x 2 dates x 16 <= 64 terms: one per lane
 __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const int32_t* k_out,
                                                             const int32_t* books,
                                                             const int32_t* upos,
                                                             const int64_t* usize, int32_t* rec,
                                                             int32_t* rlen, const int32_t* idx,
-                                                            int64_t seq) {
+                                                            int64_t seq, const int32_t* rest) {
     __shared__ int pos_s[kMaxTerms], code_s[kMaxTerms], pos_o[kMaxTerms], code_o[kMaxTerms];
     __shared__ int key_s[kMaxTerms], dep[kMaxTerms], lch[kMaxTerms], rch[kMaxTerms];
     __shared__ int hgt[kMaxTerms], newid[kMaxTerms], lcount[kMaxLevels + 1];
     __shared__ int cnt, nlev;
-    const int64_t i = blockIdx.x;
+    const int nrest = rest[0];                       // the steps turnover_terms_wave_kernel left
+    for (int j = blockIdx.x; j < nrest; j += gridDim.x) {       // (uniform per workgroup)
+    const int64_t i = rest[1 + j];
     const int tid = threadIdx.x;
     int32_t* R = rec + i * kRec;
+    __syncthreads();                                 // the previous step's LDS reads are done
     if (tid == 0) cnt = 0;
     __syncthreads();
     const int64_t si = idx ? idx[i] : i;             // book slots of this and the previous step
@@ -1681,9 +1692,9 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
             R[3] = 0;
             rlen[i] = 4;
         }
-        return;
+        continue;
     }
-    if (tid <= kMaxLevels) lcount[tid] = 0;
+    for (int l = tid; l <= kMaxLevels; l += 64) lcount[l] = 0;
     __syncthreads();
     for (int k = tid; k < ni; k += 64) atomicAdd(&lcount[hgt[k]], 1);
     __syncthreads();
@@ -1708,10 +1719,196 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
         R[4 + m + newid[k]] = na | (nb << 16);
     }
     for (int l = tid; l < L; l += 64) R[4 + m + ni + l] = lcount[l + 1];   // cumulative ends
+    }
 }
 
+// One wave per step (books of <= kWaveK names): lane e < 2 kp holds the previous step's member e,
+// lane 32 + e this step's member e; a member's term is its |cur - new| slot in the union (KKT:839).
+// Every stage runs lane-parallel in registers (no LDS, no barrier), with loops over set lanes or
+// over depth / level values instead of over all 64 lanes:
+//  - membership: one readlane loop over the members of both dates;
+//  - in-order rank: a readlane loop over the valid terms, then ds_permute to the sorted lane;
+//  - Cartesian tree: the depths are LCA depths of one real tree, so two nodes of equal depth have
+//    a shallower node between them -- the nearest not-deeper node on each side is the nearest
+//    strictly shallower one, found by ballots over the depth values in ascending order; a
+//    node's parent is the deeper of the two, and the children are scattered to their parent's
+//    lane with ds_permute (the same tree turnover_terms_kernel builds by interval scans);
+//  - heights: relaxation as in turnover_terms_kernel; level order: one ballot per level.
+__device__ __forceinline__ int wv_read(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ int wv_pull(int v, int src) {           // v of lane src (any lane)
+    return __builtin_amdgcn_ds_bpermute(src << 2, v);
+}
+__device__ __forceinline__ int wv_push(int v, int dst) {           // v to lane dst (others: 0)
+    return __builtin_amdgcn_ds_permute(dst << 2, v);
+}
+__device__ __forceinline__ int wv_min(int v) {
+    for (int o = 32; o >= 1; o >>= 1) { const int x = __shfl_xor(v, o, 64); v = x < v ? x : v; }
+    return v;
+}
+__device__ __forceinline__ int wv_max(int v) {
+    for (int o = 32; o >= 1; o >>= 1) { const int x = __shfl_xor(v, o, 64); v = x > v ? x : v; }
+    return v;
+}
+// rest[0] counts the steps left to turnover_terms_kernel (a book over kWaveK names), rest[1 + j]
+// lists them.  n < 2^31 (the hosts check).
+__global__ __launch_bounds__(256) void turnover_terms_wave_kernel(int64_t nd, const int32_t* k_out,
+                                                                  const int32_t* books,
+                                                                  const int32_t* upos,
+                                                                  const int64_t* usize,
+                                                                  int32_t* rec, int32_t* rlen,
+                                                                  const int32_t* idx, int64_t seq,
+                                                                  int32_t* rest) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t above = lane < 63 ? (~0ull << (lane + 1)) : 0ull;
+    const uint32_t useq = (uint32_t)seq;
+    const int nwv = (int)(gridDim.x * (blockDim.x >> 6));
+    for (int i = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); i < (int)nd; i += nwv) {
+        const bool first = (uint32_t)i % useq == 0;
+        const int si = idx ? idx[i] : i;
+        const int sp = first ? -1 : (idx ? idx[i - 1] : i - 1);
+        const int k = k_out[si], kp = sp >= 0 ? k_out[sp] : 0;
+        if (k > kWaveK || kp > kWaveK) {                           // (uniform in the wave)
+            if (lane == 0) rest[1 + atomicAdd(rest, 1)] = i;
+            continue;
+        }
+        int32_t* R = rec + (int64_t)i * kRec;
+        if (sp < 0 || kp <= 0) {                                   // current_positions.dropna().empty
+            if (lane == 0) {
+                R[0] = -1;
+                R[1] = 0;
+                R[2] = 0;
+                R[3] = 0;
+                rlen[i] = 4;
+            }
+            continue;
+        }
+        const int64_t n = usize[(int64_t)i * 2 + 0];
+        // members: lane e < 2 kp the previous books', lane 32 + e < 32 + 2 k this step's
+        const bool isp = lane < 2 * kp, isc = lane >= 32 && lane - 32 < 2 * k;
+        int a = -1, side = 0, pz = -1;
+        if (isp) {        // a previous member predicted today: |pos_old - pos_new| at its new slot
+            side = lane >= kp;
+            const int q = lane - side * kp;
+            a = books[((int64_t)sp * 2 + side) * kMaxK + q];
+            pz = upos[((((int64_t)i - 1) * 2 + side) * 2 + 1) * kMaxK + q];
+        }
+        if (isc) {        // a member predicted yesterday only (not in yesterday's books)
+            side = lane - 32 >= k;
+            const int q = lane - 32 - side * k;
+            a = books[((int64_t)si * 2 + side) * kMaxK + q];
+            pz = upos[(((int64_t)i * 2 + side) * 2 + 0) * kMaxK + q];
+        }
+        int ns = 2;
+        bool inprev = false;
+        for (uint64_t b = __ballot(isp || isc); b; b &= b - 1) {   // (uniform loop)
+            const int j = __builtin_ctzll(b);
+            const int aj = wv_read(a, j), sj = wv_read(side, j);
+            if (aj == a) {
+                if (j >= 32) ns = sj;
+                else inprev = true;
+            }
+        }
+        const int code = isp ? side * 3 + ns : 2 * 3 + side;
+        const bool valid = (isp || (isc && !inprev)) && pz >= 0;
+        const uint64_t vm = __ballot(valid);
+        const int m = __popcll(vm);
+        const int key = valid ? np_key(n, pz) : 0x7fffffff;
+        // rank by key among the valid lanes (keys of distinct slots are distinct); the invalid
+        // lanes take the ranks after them, in lane order
+        int r = 0;
+        for (uint64_t b = vm; b; b &= b - 1) r += wv_read(key, __builtin_ctzll(b)) < key ? 1 : 0;
+        if (!valid) r = m + __popcll(~vm & below);
+        const int pos_o = wv_push(pz, r);
+        const int code_o = wv_push(code, r);
+        // internal node kk (kk < m - 1) = the LCA of in-order terms kk and kk + 1
+        const int ni = m > 1 ? m - 1 : 0;
+        const bool node = lane < ni;
+        const int pnext = wv_pull(pos_o, lane < 63 ? lane + 1 : 63);
+        const int dep = node ? np_lca_depth(n, pos_o, pnext) : 0x3fffffff;
+        // nearest strictly shallower node on each side (-1: none)
+        int nl = -1, nr = -1;
+        {
+            const int dlo = wv_min(dep), dhi = wv_max(node ? dep : -1);
+            uint64_t sh = 0;                                       // nodes shallower than d
+            for (int d = dlo; d <= dhi; ++d) {
+                const bool at = node && dep == d;
+                const uint64_t e = __ballot(at);
+                if (e == 0) continue;
+                if (at) {
+                    const uint64_t lm = sh & below, rm = sh & above;
+                    nl = lm ? 63 - __builtin_clzll(lm) : -1;
+                    nr = rm ? __builtin_ctzll(rm) : -1;
+                }
+                sh |= e;
+            }
+        }
+        // parent = the deeper of the two; a node is its parent's left child when the parent is on
+        // its right.  Children go to the parent's lane (id + 1; 0 = none -- a term child); the
+        // other lanes push to lane 63, never a node (ni <= 63)
+        const int dl = wv_pull(dep, nl < 0 ? 0 : nl), dr = wv_pull(dep, nr < 0 ? 0 : nr);
+        const int par = nl < 0 ? nr : nr < 0 ? nl : (dl > dr ? nl : nr);
+        const bool lchild = node && par >= 0 && par == nr, rchild = node && par >= 0 && par == nl;
+        const int lcn = wv_push(lane + 1, lchild ? par : 63);
+        const int rcn = wv_push(lane + 1, rchild ? par : 63);
+        // child ids: term t -> t, node kk -> m + kk
+        const int lch = lcn ? m + lcn - 1 : lane, rch = rcn ? m + rcn - 1 : lane + 1;
+        // heights (the DAG level of an add: 1 + its children's), relaxed until they settle
+        int h = node ? 1 : 0;
+        for (int it = 0; it < ni + 1; ++it) {
+            const int ha = wv_pull(h, lch < m ? 0 : lch - m), hb = wv_pull(h, rch < m ? 0 : rch - m);
+            const int ca = lch < m ? 0 : ha, cb = rch < m ? 0 : hb;
+            const int hn = node ? (ca > cb ? ca : cb) + 1 : 0;
+            const bool ch = hn != h;
+            h = hn;
+            if (__ballot(ch) == 0ull) break;
+        }
+        const int L = wv_max(h);
+        if (L > kMaxLevels) {       // deeper than the record's level table (turnover_terms_kernel)
+            if (lane == 0) {
+                R[0] = -2;
+                R[1] = 0;
+                R[2] = 0;
+                R[3] = 0;
+                rlen[i] = 4;
+            }
+            continue;
+        }
+        // level order: the nodes of lower levels first, node order inside a level; lane l < L
+        // holds the cumulative end of level l + 1
+        int nid = 0, lend = 0, base = 0;
+        for (int l = 1; l <= L; ++l) {
+            const bool at = node && h == l;
+            const uint64_t e = __ballot(at);
+            if (at) nid = base + __popcll(e & below);
+            base += __popcll(e);
+            if (lane == l - 1) lend = base;
+        }
+        // (the pulls run on every lane: a ds_bpermute reads 0 from a lane the EXEC mask disables)
+        const int ida = wv_pull(nid, lch < m ? 0 : lch - m), idb = wv_pull(nid, rch < m ? 0 : rch - m);
+        const int na = lch < m ? lch : m + ida;
+        const int nb = rch < m ? rch : m + idb;
+        if (lane == 0) {
+            R[0] = m;
+            R[1] = ni;
+            R[2] = L;
+            R[3] = 0;
+            rlen[i] = 4 + m + ni + L;
+        }
+        if (lane < m) R[4 + lane] = code_o;
+        if (node) R[4 + m + nid] = na | (nb << 16);
+        if (lane < L) R[4 + m + ni + lane] = lend;
+    }
+}
+
+// staging of the scan: dates per chunk and record words per buffer.  The single sequence (the
+// headline) stages 64 dates in 156 KB of LDS; a bootstrap path (config E: 1,024 workgroups) stages
+// 8 in 31 KB, so five paths share a CU and all of them run in one round (round 5: 156 KB kept one
+// path per CU, four rounds).  A buffer holds at least one record (kRec words).
 constexpr int kChunkDates = 64;
 constexpr int kBufWords = 12288;
+constexpr int kPathChunkDates = 8;
+constexpr int kPathBufWords = 2048;
 
 // x / d from r = RN(1 / d) (Markstein: q0 = RN(x r), e = fma(-q0, d, x), q = RN(q0 + e r) is the
 // IEEE quotient when r is the correctly rounded reciprocal and nothing under- or overflows; the
@@ -1738,6 +1935,7 @@ __device__ __forceinline__ double mdiv(double x, double d, double r) {
 // order, so a level's reads see the previous level's writes.
 // Workgroup b scans the steps [b * nd, (b + 1) * nd) (bootstrap path b; one workgroup for the
 // plain sequence); the sums of step i are those of book slot ix(i).
+template <int kChunkDates, int kBufWords>
 __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double* sums,
                                                       const int32_t* rec, const int32_t* rlen,
                                                       double v0, double rate, double* value,
@@ -1778,7 +1976,8 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
             const int x = __shfl_up(incl, o, 64);
             if (lane >= o) incl += x;
         }
-        const bool fits = (i0 + lane < nd) && incl <= kBufWords;
+        static_assert(kBufWords >= kRec && kChunkDates <= 64, "a chunk holds 1..64 records");
+        const bool fits = (i0 + lane < nd) && lane < kChunkDates && incl <= kBufWords;
         const u64 fm = __ballot(fits);
         const int c = fm == ~0ull ? 64 : __builtin_ctzll(~fm);   // prefix of dates that fits
         // the records' first 128 words for 16 dates at a time, every load issued before the LDS
@@ -2083,6 +2282,26 @@ __global__ __launch_bounds__(256) void hist_transpose_kernel(int64_t lda, int64_
     }
 }
 
+// the turnover DAG records of n steps: the one-wave kernel for the steps with books of <= kWaveK
+// names, the persistent LDS kernel for the steps it lists in rest (n + 1 words of scratch)
+static hipError_t launch_turnover_terms(afm_ctx* ctx, int64_t n, const int32_t* k_out,
+                                        const int32_t* books, const int32_t* upos,
+                                        const int64_t* usize, int32_t* rec, int32_t* rlen,
+                                        const int32_t* idx, int64_t seq, int32_t* rest) {
+    const int64_t ncu = afm_ctx_cus(ctx);
+    hipError_t e = hipMemsetAsync(rest, 0, sizeof(int32_t), ctx->stream);
+    if (e != hipSuccess) return e;
+    const int64_t gw = std::min<int64_t>((n + 3) / 4, 8 * ncu);           // 4 waves per workgroup
+    hipLaunchKernelGGL(turnover_terms_wave_kernel, dim3((unsigned)gw), dim3(256), 0, ctx->stream, n,
+                       k_out, books, upos, usize, rec, rlen, idx, seq, rest);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t gl = std::min<int64_t>(n, 4 * ncu);
+    hipLaunchKernelGGL(turnover_terms_kernel, dim3((unsigned)gl), dim3(64), 0, ctx->stream, n, k_out,
+                       books, upos, usize, rec, rlen, idx, seq, (const int32_t*)rest);
+    return hipGetLastError();
+}
+
 template <int KM>
 static int launch_rebalance(afm_ctx* ctx, const RebArgs& r) {
     const size_t smem = sizeof(Shared<KM>);
@@ -2175,13 +2394,15 @@ extern "C" int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out,
                       short_ret, "null buffer");
     if (nd <= 0) return AFM_OK;
     int32_t* work = nullptr;
-    AFM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * (size_t)nd * (kRec + 1), ctx->stream));
+    AFM_CHECK_ARG(nd <= 0x7fffffff, "nd too large for one launch");
+    AFM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * ((size_t)nd * (kRec + 2) + 1),
+                           ctx->stream));
     int32_t* rec = work;
     int32_t* rlen = work + nd * kRec;
-    hipLaunchKernelGGL(turnover_terms_kernel, dim3((unsigned)nd), dim3(64), 0, ctx->stream, nd,
-                       k_out, books, upos, usize, rec, rlen, (const int32_t*)nullptr, nd);
-    AFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(pnl_scan_kernel, dim3(1), dim3(128), 0, ctx->stream, nd, sums, rec, rlen, v0,
+    AFM_HIP(launch_turnover_terms(ctx, nd, k_out, books, upos, usize, rec, rlen, nullptr, nd,
+                                  rlen + nd));
+    hipLaunchKernelGGL((pnl_scan_kernel<kChunkDates, kBufWords>), dim3(1), dim3(128), 0, ctx->stream,
+                       nd, sums, rec, rlen, v0,
                        rate, value, turnover, long_ret, short_ret, (const int32_t*)nullptr);
     AFM_HIP(hipGetLastError());
     AFM_HIP(hipFreeAsync(work, ctx->stream));
@@ -2217,9 +2438,10 @@ extern "C" int afm_bootstrap_pnl_f64(afm_ctx* ctx, int64_t lda, const int32_t* d
     if (n == 0) return AFM_OK;
     AFM_CHECK_ARG(n <= 0x7fffffff, "npaths * steps too large for one launch");
     const int64_t nw = lda / 64;
-    // scratch: pbits [nd][nw] u64, upos [n][2][2][kMaxK], usize [n][2], rec [n][kRec], rlen [n]
+    // scratch: pbits [nd][nw] u64, upos [n][2][2][kMaxK], usize [n][2], rec [n][kRec], rlen [n],
+    // rest [n + 1]
     const size_t b_pb = sizeof(uint64_t) * nd * nw, b_up = sizeof(int32_t) * n * 4 * kMaxK,
-                 b_us = sizeof(int64_t) * n * 2, b_rec = sizeof(int32_t) * n * (kRec + 1);
+                 b_us = sizeof(int64_t) * n * 2, b_rec = sizeof(int32_t) * (n * (kRec + 2) + 1);
     char* work = nullptr;
     AFM_HIP(hipMallocAsync((void**)&work, b_pb + b_up + b_us + b_rec, ctx->stream));
     uint64_t* pbits = (uint64_t*)work;
@@ -2233,10 +2455,10 @@ extern "C" int afm_bootstrap_pnl_f64(afm_ctx* ctx, int64_t lda, const int32_t* d
     hipLaunchKernelGGL(pair_union_kernel, dim3((unsigned)n), dim3(64), 0, ctx->stream, steps,
                        path, nw, pbits, k_out, books, upos, usize);
     AFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(turnover_terms_kernel, dim3((unsigned)n), dim3(64), 0, ctx->stream, n,
-                       k_out, books, upos, usize, rec, rlen, path, steps);
-    AFM_HIP(hipGetLastError());
-    hipLaunchKernelGGL(pnl_scan_kernel, dim3((unsigned)npaths), dim3(128), 0, ctx->stream, steps,
+    AFM_HIP(launch_turnover_terms(ctx, n, k_out, books, upos, usize, rec, rlen, path, steps,
+                                  rlen + n));
+    hipLaunchKernelGGL((pnl_scan_kernel<kPathChunkDates, kPathBufWords>), dim3((unsigned)npaths),
+                       dim3(128), 0, ctx->stream, steps,
                        sums, rec, rlen, v0, rate, value, turnover, long_ret, short_ret, path);
     AFM_HIP(hipGetLastError());
     AFM_HIP(hipFreeAsync(work, ctx->stream));
