@@ -8,6 +8,24 @@
 #include <string>
 #include <unordered_map>
 
+// Issue priority of the latency-bound tail kernels (rebalance, turnover / PnL scan, analyzer, FM
+// solve) that run beside the FM Grams' MFMA and producer waves: at equal priority the older waves
+// win every arbitration on a shared SIMD (MI355X_MICROARCH.md, two waves per SIMD).
+#ifndef AFM_TAIL_PRIO
+#define AFM_TAIL_PRIO 3
+#endif
+#ifndef AFM_SCAN_PRIO                  // the serial PnL scan and its turnover records
+#define AFM_SCAN_PRIO 3
+#endif
+#define AFM_TAIL_PRIO_SET()                                                   \
+    do {                                                                      \
+        if (AFM_TAIL_PRIO) __builtin_amdgcn_s_setprio(AFM_TAIL_PRIO);         \
+    } while (0)
+#define AFM_SCAN_PRIO_SET()                                                   \
+    do {                                                                      \
+        if (AFM_SCAN_PRIO) __builtin_amdgcn_s_setprio(AFM_SCAN_PRIO);         \
+    } while (0)
+
 #include "afm.h"
 
 struct afm_ctx {

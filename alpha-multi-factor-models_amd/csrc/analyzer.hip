@@ -219,6 +219,7 @@ struct PrepShared {
 // level, the buffers added one by one onto 0.0: mean = sum / n bit-exactly, with no serial
 // walk.  Finally the rows surviving all three steps are written compacted with demeaned returns.
 __global__ __launch_bounds__(kPT) void xs_prepare_kernel(PrepArgs g) {
+    AFM_TAIL_PRIO_SET();
     __shared__ PrepShared sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t t = g.t0 + blockIdx.x;
@@ -504,6 +505,7 @@ __device__ __forceinline__ int layer_of(int r, int n) {
 }
 
 __global__ __launch_bounds__(kLT) void xs_layers_kernel(RankArgs g) {
+    AFM_TAIL_PRIO_SET();
     __shared__ LayerSmem sh;
     const int tid = threadIdx.x, lane = tid & 63;
     const int64_t t = blockIdx.x;
@@ -737,6 +739,7 @@ struct StatArgs {
 constexpr int kStatRows = 512;
 
 __global__ __launch_bounds__(128) void xs_stats_kernel(StatArgs g) {
+    AFM_TAIL_PRIO_SET();
     __shared__ double sv[4][kStatRows];          // factor, return_1, return_2, return_5
     __shared__ int8_t slay[kStatRows];
     __shared__ double sinv[kStatRows];           // 1 / (row number): the Welford divisor when no
@@ -950,6 +953,7 @@ __global__ __launch_bounds__(1024) void xs_series_kernel(int64_t nd, const doubl
                                                          int year0, double* cum_layer, double* ls,
                                                          double* cum_port, double* ir,
                                                          double* scratch) {
+    AFM_TAIL_PRIO_SET();
     extern __shared__ double ir_lds[];                     // [3 * nyears][kSerYearCap]
     const int tid = threadIdx.x;
     if (tid < 30) {                                        // (type, layer) cumsum, NaN-skipping

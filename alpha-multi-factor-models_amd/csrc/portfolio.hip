@@ -1254,6 +1254,7 @@ __global__ __launch_bounds__(kT) void weights_kernel(const double* R, int64_t ro
 // book (k largest predictions), side 1 the short book (k smallest).
 template <int KM>
 __global__ __launch_bounds__(kT) void rebalance_kernel(RebArgs r) {
+    AFM_TAIL_PRIO_SET();
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     Shared<KM>& sh = *reinterpret_cast<Shared<KM>*>(smem_raw);
     const int tid = threadIdx.x;
@@ -1579,6 +1580,7 @@ __global__ __launch_bounds__(64) void turnover_terms_kernel(int64_t nd, const in
                                                             const int64_t* usize, int32_t* rec,
                                                             int32_t* rlen, const int32_t* idx,
                                                             int64_t seq, const int32_t* rest) {
+    AFM_SCAN_PRIO_SET();
     __shared__ int pos_s[kMaxTerms], code_s[kMaxTerms], pos_o[kMaxTerms], code_o[kMaxTerms];
     __shared__ int key_s[kMaxTerms], dep[kMaxTerms], lch[kMaxTerms], rch[kMaxTerms];
     __shared__ int hgt[kMaxTerms], newid[kMaxTerms], lcount[kMaxLevels + 1];
@@ -1758,6 +1760,7 @@ __global__ __launch_bounds__(256) void turnover_terms_wave_kernel(int64_t nd, co
                                                                   int32_t* rec, int32_t* rlen,
                                                                   const int32_t* idx, int64_t seq,
                                                                   int32_t* rest) {
+    AFM_SCAN_PRIO_SET();
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t above = lane < 63 ? (~0ull << (lane + 1)) : 0ull;
@@ -1826,10 +1829,22 @@ __global__ __launch_bounds__(256) void turnover_terms_wave_kernel(int64_t nd, co
         const bool node = lane < ni;
         const int pnext = wv_pull(pos_o, lane < 63 ? lane + 1 : 63);
         const int dep = node ? np_lca_depth(n, pos_o, pnext) : 0x3fffffff;
-        // nearest strictly shallower node on each side (-1: none)
+        // nearest strictly shallower node on each side (-1: none).  The depths of one summation
+        // tree span < 4 kMaxLevels values; a wider span means union positions that do not belong
+        // to this step's union (inconsistent inputs): an error record, not a long loop
         int nl = -1, nr = -1;
+        const int dlo = wv_min(dep), dhi = wv_max(node ? dep : -1);
+        if (dhi - dlo >= 4 * kMaxLevels) {
+            if (lane == 0) {
+                R[0] = -2;
+                R[1] = 0;
+                R[2] = 0;
+                R[3] = 0;
+                rlen[i] = 4;
+            }
+            continue;
+        }
         {
-            const int dlo = wv_min(dep), dhi = wv_max(node ? dep : -1);
             uint64_t sh = 0;                                       // nodes shallower than d
             for (int d = dlo; d <= dhi; ++d) {
                 const bool at = node && dep == d;
@@ -1941,6 +1956,7 @@ __global__ __launch_bounds__(128) void pnl_scan_kernel(int64_t nd, const double*
                                                       double v0, double rate, double* value,
                                                       double* turnover, double* long_ret,
                                                       double* short_ret, const int32_t* idx) {
+    AFM_SCAN_PRIO_SET();
     __shared__ int buf[2][kBufWords];
     __shared__ double sm[2][kChunkDates + 1][4];
     __shared__ double rcp[2][kChunkDates + 1][2];           // RN(1 / S[2]), RN(1 / S[3])

@@ -692,6 +692,7 @@ struct SolveArgs {
 constexpr int kMaxP = kMaxF - 2;
 
 __global__ __launch_bounds__(kThreads) void ols_solve_kernel(SolveArgs s) {
+    AFM_TAIL_PRIO_SET();
     extern __shared__ __attribute__((aligned(16))) double M[];    // packed lower triangle
     __shared__ double dsc[kMaxP + 1];
     __shared__ double dk[kMaxP];
@@ -974,6 +975,7 @@ __device__ double block_sum256(double v, double* red) {
 __global__ __launch_bounds__(256) void fama_macbeth_kernel(const double* beta, const int32_t* rank,
                                                            int64_t nseg, int k, double* mean_out,
                                                            double* t_out) {
+    AFM_TAIL_PRIO_SET();
     __shared__ double red[256];
     const int j = blockIdx.x, tid = threadIdx.x;
     double n = 0, s = 0;

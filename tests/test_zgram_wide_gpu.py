@@ -107,3 +107,46 @@ def test_zgram_per_date_wide_vs_fp64(p):
             continue
         assert got[d, 0, 0] == ref[0, 0]
         _close(got[d], ref, f"zgram p={p} date {t0 + d}")
+
+
+def _ref_raw_gram(c, t, a0, a1):
+    """fp64 D^T D of the raw FM design D = [1, x, y] over the kept rows of date t, assets
+    [a0, a1)."""
+    aa = np.nonzero(c["keep"][t, a0:a1])[0] + a0
+    X = c["np_base"][c["np_cols"]][:, t, aa]
+    y = c["np_base"][c["ycol"]][t, aa]
+    D = np.concatenate([np.ones((1, len(aa))), X, y[None]], axis=0)
+    return D @ D.T
+
+
+@pytest.mark.parametrize("p", [30, 17, 5])
+def test_fm_raw_per_date_gram_vs_fp64(p):
+    """afm_zgram_f64 without z statistics (the FM30 per-date Grams of KKT:630-631), per (date,
+    128-asset block) partial, against fp64 numpy; a block past a_end (an all-zero partial), an
+    empty date, a ragged block."""
+    import torch
+    from afm import _lib
+    L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+    c = _case(p, seed=2000 + p)
+    pe = L.afm_zgram_part_bytes(p) // 8
+    t0, nt, nblk, blk = 30, 24, 3, 128                   # block 2 lies past a_end = 229
+    part = torch.full((nt * nblk, pe), float("nan"), dtype=torch.float64, device="cuda")
+    G = torch.empty((nt * nblk, p + 2, p + 2), dtype=torch.float64, device="cuda")
+    h = _lib.Context.get(0).bind_stream()
+    chk(L.afm_zgram_f64(h, P(c["base"]), T * LDA, LDA, P(c["cols"]), None, p, c["ycol"],
+                        None, 0, P(c["bits"]), t0, nt, nblk, 0, blk, A_END, P(part), 0),
+        "zgram fm")
+    chk(L.afm_gram_tree_f64(h, p, P(part), nt * nblk, 1, 1, P(G)), "tree")
+    torch.cuda.synchronize()
+    got = G.cpu().numpy().reshape(nt, nblk, p + 2, p + 2)
+    for d in range(nt):
+        for b in range(nblk):
+            a0, a1 = b * blk, min((b + 1) * blk, A_END)
+            g = got[d, b]
+            if a1 <= a0 or not c["keep"][t0 + d, a0:a1].any():
+                assert (g == 0).all(), (d, b)
+                continue
+            ref = _ref_raw_gram(c, t0 + d, a0, a1)
+            assert g[0, 0] == ref[0, 0]                  # the row count is exact
+            _close(g, ref, f"fm p={p} date {t0 + d} block {b}")
+            assert np.array_equal(g, g.T)
