@@ -40,6 +40,8 @@
 // Algorithmic traffic per present asset-day: 32 B of inputs read + 98 x 8 B written = 816 B.
 #include "afm_internal.h"
 
+#include <type_traits>
+
 #include <cstdlib>
 
 #pragma clang fp contract(off)
@@ -89,12 +91,18 @@ struct Smem {
 //    num / den for chunk c during chunk c + 1 (after the barrier between them).
 // 140 KB: one workgroup per CU (the launch sizes its grid to <= the CU count).
 constexpr int kRingR = 32;           // lookbacks 0..15 + two chunks of look-ahead
-constexpr int kCorrs = 2;            // corr_5, corr_15
+constexpr int kXSlots = 2;           // exchange slots of one workgroup
+// Combiner kinds (Comb<K>): the column num / den of the previous chunk -- 0: corr_5, 1: corr_15
+// (PartS, PartT), 2: sd5_15, 3: volsd5_15 (PartT); kind k uses exchange slot k & 1, so a workgroup
+// may hold kinds 0 and 1, or 2 and 3 (the partitions place them so)
+constexpr int kCombs = 4;
+constexpr int comb_col(int k) { return k == 0 ? 94 : k == 1 ? 95 : k == 2 ? 88 : 92; }
+constexpr int comb_slot(int k) { return k & 1; }
 struct SmemRG : Smem {
     double r[kRingR][kLanes];
     double g[kRingR][kLanes];
-    double xnum[kCorrs][2][kChunk][kLanes];
-    double xden[kCorrs][2][kChunk][kLanes];
+    double xnum[kXSlots][2][kChunk][kLanes];
+    double xden[kXSlots][2][kChunk][kLanes];
 };
 
 // ---- clean windows ----------------------------------------------------------------------------
@@ -859,6 +867,7 @@ struct PvtObvPsy {  // No-talib.py:62-69
 
 template <int W, int COL>
 struct RetSd {  // sd_W of close.pct_change() (No-talib.py:72-74)
+    static constexpr int kCol = COL;
     static constexpr u64 kC = 0, kV = 0, kRt = lb(0) | lb(W), kGc = 0;
     RollVar v;
     __device__ void init() { v.init(); }
@@ -919,6 +928,7 @@ struct RetSd5x15 {  // sd_5, sd_15, sd5_15
 
 template <int W, int COL>
 struct VolSd {  // volsd_W (No-talib.py:79-80)
+    static constexpr int kCol = COL;
     static constexpr u64 kC = 0, kV = lb(0) | lb(W);
     static constexpr u64 kRt = 0, kGc = 0;
     RollVar v;
@@ -976,6 +986,29 @@ struct VolSd5x15 {
         double x = a.wstep(s), y = b.wstep(s);
         s.put(92, x / y);
     }
+};
+
+// sd5_15 / volsd5_15 split over two waves (PartT): the sd_5 wave writes its value of every present
+// day into exchange slot SLOT's numerator (NUM), the sd_15 wave into its denominator, and the wave
+// holding Comb<2> / Comb<3> stores x / y one chunk later -- the division RetSd5x15 / VolSd5x15
+// make, on the same values, so columns 88 / 92 are bit-identical (and their NaN bits are the
+// combiner's).  J = RetSd<W, COL> or VolSd<W, COL>; the sd column itself is stored as in the
+// unsplit job.
+template <class J, int SLOT, bool NUM>
+struct XSd {
+    static constexpr u64 kC = J::kC, kV = J::kV, kRt = J::kRt, kGc = J::kGc;
+    static constexpr Cols kOut = col1(J::kCol);
+    J a;
+    template <class S> __device__ __forceinline__ static void xput(S& s, double v) {
+        static_assert(S::kRG, "the split ratio needs the SmemRG exchange");
+        LDS SmemRG* rg = (LDS SmemRG*)s.sm;
+        if constexpr (NUM) rg->xnum[SLOT][s.par][s.sday][s.lane] = v;
+        else rg->xden[SLOT][s.par][s.sday][s.lane] = v;
+    }
+    __device__ void init() { a.init(); }
+    template <class S> __device__ void step(S& s) { xput(s, a.step(s)); }
+    template <class S> __device__ void fstep(S& s) { xput(s, a.fstep(s)); }
+    template <class S> __device__ void wstep(S& s) { xput(s, a.wstep(s)); }
 };
 
 // ret.rolling(W).corr(vol_change) (No-talib.py:85-87; pandas Rolling.corr on prep_binary'd
@@ -1207,8 +1240,8 @@ struct CorrV {
     }
 };
 
-// Marks the wave that combines split correlation K (num / den of the previous chunk, its column
-// stores and NaN bits; run_wave).  No per-day work.
+// Marks the wave that combines split column K (kinds: see kCombs -- num / den of the previous
+// chunk, its column stores and NaN bits; run_wave).  No per-day work.
 template <int K>
 struct Comb {
     static constexpr u64 kC = 0, kV = 0, kRt = 0, kGc = 0;
@@ -1237,6 +1270,12 @@ template <> struct Ser<VolSd5x15> { static constexpr unsigned value = kSerVP; };
 template <int W, bool V> struct Ser<Corr<W, V>> { static constexpr unsigned value = kSerXY; };
 template <int W, bool V> struct Ser<CorrM<W, V>> { static constexpr unsigned value = kSerXY; };
 template <int W> struct Ser<CorrV<W>> { static constexpr unsigned value = kSerXY; };
+template <int W, int C, int SL, bool N> struct Ser<XSd<RetSd<W, C>, SL, N>> {
+    static constexpr unsigned value = kSerR;
+};
+template <int W, int C, int SL, bool N> struct Ser<XSd<VolSd<W, C>, SL, N>> {
+    static constexpr unsigned value = kSerVP;
+};
 
 template <class... J>
 struct Pack;
@@ -1295,6 +1334,7 @@ struct Pack<H, R...> {
 struct PartC {
     static constexpr int kSets = 15;
     static constexpr bool kRG = false;
+    static constexpr int kCombs = 0;
     template <int K> struct Set;
 };
 #ifdef AFM_FP_CENSUS_W0     // instruction census of one job alone (tools/job_census.sh)
@@ -1328,6 +1368,7 @@ template <> struct PartC::Set<14> { using type = Pack<Bbands<26>, Vwma<26>, Ema<
 struct PartS {
     static constexpr int kSets = 30;
     static constexpr bool kRG = true;
+    static constexpr int kCombs = 2;                  // corr_5, corr_15
     template <int K> struct Set;
 };
 template <> struct PartS::Set<0> { using type = Pack<CorrM<5, true>, Ema<6>>; };
@@ -1361,8 +1402,83 @@ template <> struct PartS::Set<27> { using type = Pack<Rsi<14>, VolSd3, Ema<26>>;
 template <> struct PartS::Set<28> { using type = Pack<Rsi<20>, PvtObvPsy>; };
 template <> struct PartS::Set<29> { using type = Pack<Macd<18>, Macd<24>, Macd<30>, Ema<46>, Ema<50>, Sma<46>, Sma<50>>; };
 
+// PartT (the smallest grids: up to 42 blocks, the N = 8 / N = 4 shards; round 5): 60 job sets of
+// ONE recurrence family each (a few pairs of light ones), J = 5, 6 or 10 job waves + a loader per
+// 140-KB workgroup -- at 20 blocks 240 workgroups of 5 job waves, ~1.2 job waves per SIMD, each
+// set's per-day chain about half PartS's.  Besides the correlations, sd5_15 and volsd5_15 are
+// split too (XSd: the sd_5 and sd_15 waves feed exchange slots 0 / 1 of their workgroup, Comb<2>
+// / Comb<3> divide).  Sets 0-4 (the correlations and their combiners) and 30-34 (the sd ratios)
+// lie inside one workgroup for every J, and each of those workgroups uses exchange slots 0 and 1
+// once.  Light sets sit at positions 0 and 4 of a 5-wave group (they share SIMD 0).
+struct PartT {
+    static constexpr int kSets = 60;
+    static constexpr bool kRG = true;
+    static constexpr int kCombs = 4;                  // corr_5, corr_15, sd5_15, volsd5_15
+    template <int K> struct Set;
+};
+template <> struct PartT::Set<0> { using type = Pack<CorrM<5, true>>; };
+template <> struct PartT::Set<1> { using type = Pack<CorrV<5>>; };
+template <> struct PartT::Set<2> { using type = Pack<CorrM<15, false>>; };
+template <> struct PartT::Set<3> { using type = Pack<CorrV<15>>; };
+template <> struct PartT::Set<4> { using type = Pack<Comb<0>, Comb<1>, Ema<6>>; };
+template <> struct PartT::Set<5> { using type = Pack<Bbands<14>>; };
+template <> struct PartT::Set<6> { using type = Pack<Vwma<6>>; };
+template <> struct PartT::Set<7> { using type = Pack<Bbands<20>>; };
+template <> struct PartT::Set<8> { using type = Pack<Vwma<10>>; };
+template <> struct PartT::Set<9> { using type = Pack<Sma<6>>; };
+template <> struct PartT::Set<10> { using type = Pack<Bbands<26>>; };
+template <> struct PartT::Set<11> { using type = Pack<Vwma<14>>; };
+template <> struct PartT::Set<12> { using type = Pack<Bbands<32>>; };
+template <> struct PartT::Set<13> { using type = Pack<Vwma<18>>; };
+template <> struct PartT::Set<14> { using type = Pack<Sma<10>>; };
+template <> struct PartT::Set<15> { using type = Pack<Bbands<38>>; };
+template <> struct PartT::Set<16> { using type = Pack<Vwma<22>>; };
+template <> struct PartT::Set<17> { using type = Pack<Bbands<44>>; };
+template <> struct PartT::Set<18> { using type = Pack<Vwma<26>>; };
+template <> struct PartT::Set<19> { using type = Pack<Sma<14>>; };
+template <> struct PartT::Set<20> { using type = Pack<Bbands<50>>; };
+template <> struct PartT::Set<21> { using type = Pack<Vwma<30>>; };
+template <> struct PartT::Set<22> { using type = Pack<Bbands<56>>; };
+template <> struct PartT::Set<23> { using type = Pack<Vwma<34>>; };
+template <> struct PartT::Set<24> { using type = Pack<Sma<18>>; };
+template <> struct PartT::Set<25> { using type = Pack<Rsi<8>>; };
+template <> struct PartT::Set<26> { using type = Pack<Vwma<38>>; };
+template <> struct PartT::Set<27> { using type = Pack<Rsi<14>>; };
+template <> struct PartT::Set<28> { using type = Pack<Vwma<42>>; };
+template <> struct PartT::Set<29> { using type = Pack<Sma<22>>; };
+template <> struct PartT::Set<30> { using type = Pack<XSd<RetSd<5, 86>, 0, true>>; };
+template <> struct PartT::Set<31> { using type = Pack<XSd<RetSd<15, 87>, 0, false>>; };
+template <> struct PartT::Set<32> { using type = Pack<XSd<VolSd<5, 90>, 1, true>>; };
+template <> struct PartT::Set<33> { using type = Pack<XSd<VolSd<15, 91>, 1, false>>; };
+template <> struct PartT::Set<34> { using type = Pack<Comb<2>, Comb<3>, Ema<10>>; };
+template <> struct PartT::Set<35> { using type = Pack<Rsi<20>>; };
+template <> struct PartT::Set<36> { using type = Pack<Vwma<46>>; };
+template <> struct PartT::Set<37> { using type = Pack<PvtObvPsy>; };
+template <> struct PartT::Set<38> { using type = Pack<Vwma<50>>; };
+template <> struct PartT::Set<39> { using type = Pack<Sma<26>>; };
+template <> struct PartT::Set<40> { using type = Pack<MomAccelRocr<14>>; };
+template <> struct PartT::Set<41> { using type = Pack<RetSd3, Ema<14>>; };
+template <> struct PartT::Set<42> { using type = Pack<MomAccelRocr<20>>; };
+template <> struct PartT::Set<43> { using type = Pack<VolSd3, Ema<18>>; };
+template <> struct PartT::Set<44> { using type = Pack<Sma<30>>; };
+template <> struct PartT::Set<45> { using type = Pack<MomAccelRocr<26>>; };
+template <> struct PartT::Set<46> { using type = Pack<Macd<18>, Ema<22>>; };
+template <> struct PartT::Set<47> { using type = Pack<MomAccelRocr<32>>; };
+template <> struct PartT::Set<48> { using type = Pack<Macd<24>, Ema<26>>; };
+template <> struct PartT::Set<49> { using type = Pack<Sma<34>>; };
+template <> struct PartT::Set<50> { using type = Pack<MomAccelRocr<38>>; };
+template <> struct PartT::Set<51> { using type = Pack<Macd<30>, Ema<30>>; };
+template <> struct PartT::Set<52> { using type = Pack<MomAccelRocr<44>>; };
+template <> struct PartT::Set<53> { using type = Pack<Sma<38>, Ema<34>>; };
+template <> struct PartT::Set<54> { using type = Pack<Sma<42>, Ema<38>>; };
+template <> struct PartT::Set<55> { using type = Pack<MomAccelRocr<50>>; };
+template <> struct PartT::Set<56> { using type = Pack<Sma<46>, Ema<42>>; };
+template <> struct PartT::Set<57> { using type = Pack<MomAccelRocr<56>>; };
+template <> struct PartT::Set<58> { using type = Pack<Sma<50>, Ema<46>>; };
+template <> struct PartT::Set<59> { using type = Pack<Ema<50>>; };
+
 // mask partials of a partition: one per job set + one per split correlation's combiner
-template <class Part> constexpr int nparts() { return Part::kSets + (Part::kRG ? kCorrs : 0); }
+template <class Part> constexpr int nparts() { return Part::kSets + Part::kCombs; }
 
 // The loader wave: global -> ring, one chunk ahead.  Executes the same barrier sequence as the
 // job waves (one per chunk).  It also publishes, per lane and chunk, whether every present day of
@@ -1379,8 +1495,12 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
     LDS SmemRG* rg = (LDS SmemRG*)smp;
     const int64_t asset = block * kLanes + lane_asset(lane);
     const int c0 = a.c0, nch = a.c1;
-    double pc[kChunk], pv[kChunk];
-    u64 vb = a.vbits[(int64_t)((c0 * kChunk) >> 6) * a.lda + asset];
+    // kPre chunks of loads in flight (round 5: with one, the loader's load latency bounded every
+    // small-grid workgroup at ~4.9 Mcycles -- ~970 cycles per day -- whatever its job sets,
+    // profiles/r5_s_wave_profiles.txt)
+    constexpr int kPre = 3;
+    double pc[kPre][kChunk], pv[kPre][kChunk];
+    u64 pw[kPre];                                   // each staged chunk's presence word
     int pmod = 0;                                   // observations before the staged chunk, mod kRing
     int run = 0;                                    // consecutive in-range observations (cap kClean)
     int cnt = 0;                                    // observations (capped at kClean)
@@ -1408,36 +1528,45 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         cprev = sm.c[q][lane];
         vprev = sm.v[q][lane];
     }
-    auto load = [&](int ch) {
+    // Every load is issued on every path -- a chunk past the slab re-reads the slab's last chunk,
+    // a date past t1 re-reads row t1 - 1, values that are never staged -- and consumed only when
+    // staged: a load consumed where it is issued, or issued under a condition, makes the compiler
+    // wait for the whole prefetch there ("compiler waits")
+    auto load = [&](int ch, double (&xc)[kChunk], double (&xv)[kChunk], u64& w) {
+        const int chc = ch < nch ? ch : nch - 1;
+        w = a.vbits[(int64_t)((chc * kChunk) >> 6) * a.lda + asset];
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
-            const int64_t t = (int64_t)ch * kChunk + j;
-            const bool in = t < a.t1;
-            pc[j] = in ? a.close[t * a.lda + asset] : 0.0;
-            pv[j] = in ? a.volume[t * a.lda + asset] : 0.0;
+            const int64_t t = (int64_t)chc * kChunk + j;
+            const int64_t tc = t < a.t1 ? t : a.t1 - 1;
+            xc[j] = a.close[tc * a.lda + asset];
+            xv[j] = a.volume[tc * a.lda + asset];
         }
     };
-    auto stage = [&](int ch) {                      // registers (chunk ch) -> ring + cbyte
+    // registers (chunk ch) -> ring + cbyte (dates past t1 stage 0: never present there, as the
+    // slabs end on a 64-date word or at T)
+    auto stage = [&](int ch, const double (&xc)[kChunk], const double (&xv)[kChunk], u64 w) {
         const int sh = (ch * kChunk) & 63;
-        if (sh == 0 && ch > c0) vb = a.vbits[(int64_t)((ch * kChunk) >> 6) * a.lda + asset];
-        const u64 cb = (vb >> sh) & 0xffull;
+        const u64 cb = (w >> sh) & 0xffull;
         int q = pmod;
         bool ok = true, warm = true;
 #pragma unroll
         for (int j = 0; j < kChunk; ++j) {
             if ((cb >> j) & 1ull) {
-                sm.c[q][lane] = pc[j];
-                sm.v[q][lane] = pv[j];
+                const bool in = (int64_t)ch * kChunk + j < a.t1;
+                const double cj = in ? xc[j] : 0.0, vj = in ? xv[j] : 0.0;
+                sm.c[q][lane] = cj;
+                sm.v[q][lane] = vj;
                 if constexpr (RG) {
-                    const double r = pc[j] / cprev - 1, g = pv[j] / vprev - 1;
+                    const double r = cj / cprev - 1, g = vj / vprev - 1;
                     rg->r[p32][lane] = cnt > 0 ? r : qnan();
                     rg->g[p32][lane] = cnt > 0 ? g : qnan();
-                    cprev = pc[j];
-                    vprev = pv[j];
+                    cprev = cj;
+                    vprev = vj;
                     p32 = (p32 + 1) & (kRingR - 1);
                 }
                 q = q + 1 == kRing ? 0 : q + 1;
-                const bool good = pc[j] > kLo && pc[j] < kHi && pv[j] > kLo && pv[j] < kHi;
+                const bool good = cj > kLo && cj < kHi && vj > kLo && vj < kHi;
                 run = good ? (run < kClean ? run + 1 : kClean) : 0;
                 cnt = cnt < kClean ? cnt + 1 : kClean;
                 ok = ok && run >= kClean;
@@ -1448,16 +1577,26 @@ __device__ __forceinline__ void load_wave(const Args& a, LDS Smem* smp, int lane
         sm.cbyte[ch & 1][lane] = (int)cb;
         sm.okbyte[ch & 1][lane] = !a.fast ? 0 : ok ? 2 : warm ? 1 : 0;
     };
-    load(c0);
-    stage(c0);
-    if (c0 + 1 < nch) load(c0 + 1);
+    static_assert(kPre == 3, "the loop below is unrolled for three buffers");
+    load(c0, pc[0], pv[0], pw[0]);
+    load(c0 + 1, pc[1], pv[1], pw[1]);
+    load(c0 + 2, pc[2], pv[2], pw[2]);
+    stage(c0, pc[0], pv[0], pw[0]);
     lds_barrier();                                  // chunk c0 staged
-    for (int ch = c0; ch < nch; ++ch) {
-        if (ch + 1 < nch) {
-            stage(ch + 1);
-            if (ch + 2 < nch) load(ch + 2);
-        }
+    // iteration ch = c0 + i: stage chunk ch + 1 (buffer (i + 1) % 3), then load chunk ch + 3 into
+    // buffer i % 3 (chunk ch's, staged one iteration ago); one barrier per chunk, as the job waves
+    auto iter = [&](int ch, auto bc) {
+        constexpr int b = decltype(bc)::value, bn = (b + 1) % kPre;
+        if (ch + 1 < nch) stage(ch + 1, pc[bn], pv[bn], pw[bn]);
+        load(ch + 3, pc[b], pv[b], pw[b]);
         lds_barrier();
+    };
+    for (int ch = c0; ch < nch; ch += kPre) {
+        iter(ch, std::integral_constant<int, 0>{});
+        if (ch + 1 >= nch) break;
+        iter(ch + 1, std::integral_constant<int, 1>{});
+        if (ch + 2 >= nch) break;
+        iter(ch + 2, std::integral_constant<int, 2>{});
     }
     if (st) {                                       // for the next slab (after the last barrier:
         for (int q = 0; q < kRing; ++q) {           // no job wave reads the ring any more)
@@ -1539,7 +1678,7 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
         pmod = js.pmod;
     }
     u64 nb = 0ull, fb = 0ull;   // this wave's NaN / non-finite bits of the current 64-day word
-    u64 cnb[kCorrs] = {0ull, 0ull}, cfb[kCorrs] = {0ull, 0ull};   // the combiner's, likewise
+    u64 cnb[kCombs] = {0ull, 0ull, 0ull, 0ull}, cfb[kCombs] = {0ull, 0ull, 0ull, 0ull};   // the combiner's
     lds_barrier();              // chunk 0 staged
 #ifdef AFM_FP_PROFILE
     const long long tstart = __builtin_readcyclecounter();
@@ -1751,23 +1890,28 @@ __device__ __forceinline__ void run_wave(const Args& a, LDS Smem* smp, int type,
             const LDS SmemRG* rg = (const LDS SmemRG*)smp;
             const int par = ch & 1, sh = (ch * kChunk) & 63;
 #pragma unroll
-            for (int k = 0; k < kCorrs; ++k) {
+            for (int k = 0; k < kCombs; ++k) {
                 if (!((KC >> k) & 1u)) continue;
-                const int col = 94 + k;
+                const int col = comb_col(k), xs = comb_slot(k);
                 GLB double* row = a.out + (int64_t)ch * kChunk * a.lda;
                 unsigned n8 = 0u, f8 = 0u;
-#pragma unroll 1
-                for (int s = 0; s < kChunk; ++s, row += a.lda) {
+                // the chunk's 8 quotients are independent: all reads and divisions first, so
+                // their latencies overlap (round 5: a one-day-at-a-time loop made a combining
+                // wave the longest of its workgroup); absent lanes' quotients are discarded
+                double xq[kChunk];
+#pragma unroll
+                for (int s = 0; s < kChunk; ++s) {
                     const bool pres = (cb >> s) & 1u;
-                    double x = qnan();
-                    if (pres) {
-                        x = rg->xnum[k][par][s][lane] / rg->xden[k][par][s][lane];
-                        n8 |= (x != x) ? 1u << s : 0u;
-                        f8 |= !__builtin_isfinite(x) ? 1u << s : 0u;
-                    }
-                    if (__builtin_amdgcn_ballot_w64(pres) != 0ull) {
+                    const double x = rg->xnum[xs][par][s][lane] / rg->xden[xs][par][s][lane];
+                    xq[s] = pres ? x : qnan();
+                    n8 |= (pres && x != x) ? 1u << s : 0u;
+                    f8 |= (pres && !__builtin_isfinite(x)) ? 1u << s : 0u;
+                }
+#pragma unroll
+                for (int s = 0; s < kChunk; ++s, row += a.lda) {
+                    if (__builtin_amdgcn_ballot_w64((cb >> s) & 1u) != 0ull) {
                         st.out = row;
-                        st.store1(col, x);
+                        st.store1(col, xq[s]);
                     }
                 }
                 cnb[k] |= (u64)n8 << sh;
@@ -1874,7 +2018,8 @@ constexpr int part_state_words() {
     if constexpr (K == Part::kSets) return loader_state_words<Part::kRG>();
     else return cmax(state_words<typename Part::template Set<K>::type>(), part_state_words<Part, K + 1>());
 }
-constexpr int kStateWords = cmax(part_state_words<PartC>(), part_state_words<PartS>());
+constexpr int kStateWords = cmax(cmax(part_state_words<PartC>(), part_state_words<PartS>()),
+                                 part_state_words<PartT>());
 
 // Job set k of a partition on this wave (a uniform branch chain; every set's code is inlined)
 template <class Part, int K = 0>
@@ -2070,18 +2215,24 @@ extern "C" int afm_debug_wave_cycles(long long* host, int n) {
 
 // The launch shape: a partition and its workgroups per block (TYPES), as one code -- PartC:
 // 1, 3, 5 or 15; PartS: 100 + TYPES with TYPES = 10, 6, 5 or 3 (J = 3, 5, 6, 10 job waves per
-// workgroup).  (The option factor_split takes the same codes.)
-//  * PartS while its 140-KB workgroups (one per CU) all fit the device at once: the fewest job
-//    waves per workgroup that do, so a small grid keeps one wave per SIMD (its per-wave chains
-//    bound it) -- the N = 8 shard (20 blocks) J = 3, configs B / D (47 blocks) J = 6, the
-//    N = 2 shard (79 blocks) J = 10.
+// workgroup); PartT: 200 + TYPES with TYPES = 12, 10 or 6 (J = 5, 6, 10).  (The option
+// factor_split takes the same codes.)
+//  * PartS / PartT while their 140-KB workgroups (one per CU) all fit the device at once: the
+//    N = 8 shard (20 blocks) PartS J = 3 (one job wave per SIMD), the N = 4 shard (40 blocks)
+//    PartT J = 10, configs B / D (47 blocks) PartS J = 6, the N = 2 shard (79 blocks) PartS J = 10.
 //  * PartC otherwise (config C, 157 blocks): the most job-set splits whose 78-KB workgroups are
 //    all resident, two per CU; 3 at least (the unsplit 16-wave workgroup caps the waves at 128
 //    VGPRs, below what the job waves need for the fast step); extra 3-way workgroups queue.
 static int factor_types(afm_ctx* ctx, int64_t nblk) {
     if (ctx->factor_split) return ctx->factor_split;               // option factor_split
     const int64_t ncu = afm_ctx_cus(ctx);
-    for (int t : {10, 6, 5, 3})
+    // PartS with one job wave per SIMD while that fits (up to 25 blocks: the N = 8 shard); then
+    // PartT with 10 job waves per workgroup (26-42 blocks: the N = 4 shard); then PartS again
+    // (measured, profiles/r5_rt_partitions.txt: at 1,250 assets PartS 2.49 ms vs PartT 2.74-3.01,
+    // at 2,500 PartT 3.27 vs PartS 3.63)
+    if (nblk * 10 <= ncu) return 110;
+    if (nblk * 6 <= ncu) return 206;
+    for (int t : {5, 3})
         if (nblk * t <= ncu) return 100 + t;
     int types = 3;
     for (int t : {5, 15})
@@ -2115,10 +2266,13 @@ static int launch_split(afm_ctx* ctx, int64_t nblk, const afm::Args& a) {
 }
 // mask partials of a launch code
 static int code_parts(int code) {
-    return code > 100 ? afm::nparts<afm::PartS>() : afm::nparts<afm::PartC>();
+    return code > 200 ? afm::nparts<afm::PartT>()
+                      : code > 100 ? afm::nparts<afm::PartS>() : afm::nparts<afm::PartC>();
 }
-static int code_types(int code) { return code > 100 ? code - 100 : code; }
-static int code_sets(int code) { return code > 100 ? afm::PartS::kSets : afm::PartC::kSets; }
+static int code_types(int code) { return code % 100; }
+static int code_sets(int code) {
+    return code > 200 ? afm::PartT::kSets : code > 100 ? afm::PartS::kSets : afm::PartC::kSets;
+}
 
 // The factor kernel over the time slab [t0, t1) of the [T]-date series (t0 a multiple of 64;
 // [0, T) = the whole series).  out / nanfree / finite hold the slab's dates only.  state: the
@@ -2189,6 +2343,7 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     int rc;
     using afm::PartC;
     using afm::PartS;
+    using afm::PartT;
     switch (code) {                  // paired 2-item workgroups for the 3-way split (see the kernel)
         case 1: rc = launch_split<PartC, 1, false>(ctx, nblk, a); break;
         case 3: rc = pair ? launch_split<PartC, 3, true>(ctx, nblk, a)
@@ -2200,6 +2355,9 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
         case 105: rc = launch_split<PartS, 5, false>(ctx, nblk, a); break;
         case 106: rc = launch_split<PartS, 6, false>(ctx, nblk, a); break;
         case 110: rc = launch_split<PartS, 10, false>(ctx, nblk, a); break;
+        case 206: rc = launch_split<PartT, 6, false>(ctx, nblk, a); break;
+        case 210: rc = launch_split<PartT, 10, false>(ctx, nblk, a); break;
+        case 212: rc = launch_split<PartT, 12, false>(ctx, nblk, a); break;
         default:
             afm_set_error("factor kernel: factor_split is not a split of the job sets");
             rc = AFM_E_ARG;

@@ -25,9 +25,11 @@ def main():
     L = _lib.lib()
     nblk = (A + 63) // 64
     # AFM_FP_TYPES: the launch code the run used (factor_split; 1xx = the 30-set partition with
-    # xx workgroups per block)
+    # xx workgroups per block, 2xx = the 60-set one)
     code = int(os.environ.get('AFM_FP_TYPES', '3'))
-    if code > 100:
+    if code > 200:
+        types, jw = code - 200, 60 // (code - 200)
+    elif code > 100:
         types, jw = code - 100, 30 // (code - 100)
     else:
         types, jw = code, 15 // code
