@@ -318,6 +318,7 @@ class Pipeline:
         self.rdates = torch.from_numpy(rd).to(dev)
         self.reb_ext = self.reb if W == 1 else reb_buffers(self.e1 - self.e0)
         self.nr_max = max(b - a for a, b in self.rrange)
+        self._reb_rows = None
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         # analyzer on the test sub-grid (64-date aligned, so the bit words line up)
@@ -688,13 +689,19 @@ class Pipeline:
                 an[k][a:b] = g[q, :b - a]
 
     def _place(self, dst, gathered, rows=None):
-        """Scatter per-rank shard columns ([W][rows][wide]) into a full-width plane."""
-        for q, (lo, hi) in enumerate(self.ranges):
-            if hi > lo:
-                if rows is None:
-                    dst[:, lo:hi] = gathered[q][:, :hi - lo]
-                else:
-                    dst[rows, lo:hi] = gathered[q][:, :hi - lo]
+        """Scatter per-rank shard columns ([W][rows][wide]) into a full-width plane.  Rank q's
+        columns start at q * wide (the fixed block split), so the ranks side by side ARE the
+        plane's first W * wide columns: one reorder copy and one copy, not one per rank (each
+        small copy is a launch the step waits on)."""
+        A = self.ranges[-1][1]
+        if A == 0:
+            return
+        W, nr, wide = gathered.shape[0], gathered.shape[1], gathered.shape[2]
+        side = gathered.permute(1, 0, 2).reshape(nr, W * wide)
+        if rows is None:
+            dst[:, :A] = side[:, :A]
+        else:
+            dst[rows, :A] = side[:, :A]
 
     def _gather_test_planes(self):
         import torch
@@ -725,9 +732,14 @@ class Pipeline:
                                   device=v.device)
                 own = torch.cat([own, pad])
             owns.append(own)
+        if self._reb_rows is None:          # gathered row (rank q, i) of every rebalance date
+            self._reb_rows = torch.as_tensor(
+                np.concatenate([q * self.nr_max + np.arange(b - a) for q, (a, b)
+                                in enumerate(self.rrange)]).astype(np.int64), device=x["k"].device)
         for k, gath in zip(x.keys(), self.comm.all_gather_packed(owns)):
-            for q, (qlo, qhi) in enumerate(self.rrange):
-                self.reb[k][qlo:qhi] = gath[q, :qhi - qlo]
+            if self.nd > 0:                 # one gather per key, not one copy per rank
+                torch.index_select(gath.reshape((-1,) + tuple(gath.shape[2:])), 0,
+                                   self._reb_rows, out=self.reb[k][:self.nd])
 
     def _fm_exchange(self):
         import torch
