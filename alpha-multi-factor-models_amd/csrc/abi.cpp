@@ -63,10 +63,10 @@ int afm_ctx_set_option(afm_ctx* ctx, const char* name, int64_t value) {
     if (n == "factor_split") {
         AFM_CHECK_ARG(value == 0 || value == 1 || value == 3 || value == 5 || value == 15 ||
                           value == 103 || value == 105 || value == 106 || value == 110 ||
-                          value == 206 || value == 210 || value == 212,
+                          value == 206,
                       "factor_split: 0 (auto); 1, 3, 5 or 15 (the 15-set partition); 103, 105, "
-                      "106 or 110 (the 30-set small-grid partition); 206, 210 or 212 (the "
-                      "60-set partition of the smallest grids)");
+                      "106 or 110 (the 30-set small-grid partition); 206 (the 60-set "
+                      "partition)");
         ctx->factor_split = (int)value;
     } else if (n == "factor_pair") {
         ctx->factor_pair = value != 0;

@@ -1402,14 +1402,14 @@ template <> struct PartS::Set<27> { using type = Pack<Rsi<14>, VolSd3, Ema<26>>;
 template <> struct PartS::Set<28> { using type = Pack<Rsi<20>, PvtObvPsy>; };
 template <> struct PartS::Set<29> { using type = Pack<Macd<18>, Macd<24>, Macd<30>, Ema<46>, Ema<50>, Sma<46>, Sma<50>>; };
 
-// PartT (the smallest grids: up to 42 blocks, the N = 8 / N = 4 shards; round 5): 60 job sets of
-// ONE recurrence family each (a few pairs of light ones), J = 5, 6 or 10 job waves + a loader per
-// 140-KB workgroup -- at 20 blocks 240 workgroups of 5 job waves, ~1.2 job waves per SIMD, each
-// set's per-day chain about half PartS's.  Besides the correlations, sd5_15 and volsd5_15 are
-// split too (XSd: the sd_5 and sd_15 waves feed exchange slots 0 / 1 of their workgroup, Comb<2>
-// / Comb<3> divide).  Sets 0-4 (the correlations and their combiners) and 30-34 (the sd ratios)
-// lie inside one workgroup for every J, and each of those workgroups uses exchange slots 0 and 1
-// once.  Light sets sit at positions 0 and 4 of a 5-wave group (they share SIMD 0).
+// PartT (26-42 blocks: the N = 4 shard; round 5): 60 job sets of ONE recurrence family each (a few
+// pairs of light ones), 10 job waves + a loader per 140-KB workgroup (6 per block).  Besides the
+// correlations, sd5_15 and volsd5_15 are split too (XSd: the sd_5 and sd_15 waves feed exchange
+// slots 0 / 1 of their workgroup, Comb<2> / Comb<3> divide).  Sets 0-4 (the correlations and
+// their combiners) and 30-34 (the sd ratios) lie inside one workgroup for J = 5, 6 and 10, and
+// each of those workgroups uses exchange slots 0 and 1 once.  Measured at 2,500 assets: 3.27 vs
+// PartS's 3.63 ms; at 1,250 it loses to PartS J = 3 (a small-grid job wave's cost is its per-day
+// fixed chain, not its jobs: profiles/r5_rt_partitions.txt), so only J = 10 is built.
 struct PartT {
     static constexpr int kSets = 60;
     static constexpr bool kRG = true;
@@ -2215,8 +2215,9 @@ extern "C" int afm_debug_wave_cycles(long long* host, int n) {
 
 // The launch shape: a partition and its workgroups per block (TYPES), as one code -- PartC:
 // 1, 3, 5 or 15; PartS: 100 + TYPES with TYPES = 10, 6, 5 or 3 (J = 3, 5, 6, 10 job waves per
-// workgroup); PartT: 200 + TYPES with TYPES = 12, 10 or 6 (J = 5, 6, 10).  (The option
-// factor_split takes the same codes.)
+// workgroup); PartT: 206 (TYPES = 6, J = 10; J = 5 / 6 measured slower than PartS at every size,
+// profiles/r5_rt_partitions.txt, and are not built).  (The option factor_split takes the same
+// codes.)
 //  * PartS / PartT while their 140-KB workgroups (one per CU) all fit the device at once: the
 //    N = 8 shard (20 blocks) PartS J = 3 (one job wave per SIMD), the N = 4 shard (40 blocks)
 //    PartT J = 10, configs B / D (47 blocks) PartS J = 6, the N = 2 shard (79 blocks) PartS J = 10.
@@ -2356,8 +2357,6 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
         case 106: rc = launch_split<PartS, 6, false>(ctx, nblk, a); break;
         case 110: rc = launch_split<PartS, 10, false>(ctx, nblk, a); break;
         case 206: rc = launch_split<PartT, 6, false>(ctx, nblk, a); break;
-        case 210: rc = launch_split<PartT, 10, false>(ctx, nblk, a); break;
-        case 212: rc = launch_split<PartT, 12, false>(ctx, nblk, a); break;
         default:
             afm_set_error("factor kernel: factor_split is not a split of the job sets");
             rc = AFM_E_ARG;

@@ -42,7 +42,7 @@ def log(*a):
 
 # per-launch HBM bytes from the latest PMC passes (tools/prof_counters.sh -> tools/pmc_traffic.py;
 # FETCH_SIZE x2 and KiB corrections of MI355X_MICROARCH.md applied there)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r4_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r5_w_pmc_traffic.json")
 ROOF_KERNELS = {"factors": ("factor_panel_kernel", "masks_kernel", "labels_kernel"),
                 "factors_nolabels": ("factor_panel_kernel", "masks_kernel"),
                 "xs_gram": ("zgram_kernel<7, 1, true>",)}

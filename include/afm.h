@@ -44,8 +44,8 @@ int afm_ctx_set_stream(afm_ctx* ctx, void* stream);
  * set them; defaults are the library's choice):
  *   "factor_split"  0 (auto) | 1 | 3 | 5 | 15: workgroups per 64-asset block of the factor kernel
  *                   (the 15-set partition) | 103 | 105 | 106 | 110: 100 + workgroups per block
- *                   of the 30-set small-grid partition | 206 | 210 | 212: 200 + workgroups per
- *                   block of the 60-set partition of the smallest grids
+ *                   of the 30-set small-grid partition | 206: 6 workgroups per block of the
+ *                   60-set partition (the N = 4 shard)
  *   "factor_pair"   1 (default) | 0: the 3-way split runs two items per workgroup
  *   "factor_fast"   1 (default) | 0: the clean-window fast step of the factor kernel
  *   "gram_checked"  0 (default) | 1: afm_xs_gram_f64 stages every row checked (no FAST + REDO) */

@@ -60,16 +60,15 @@ def test_factor_grid_vs_oracle(A, T, seed, kw):
 @pytest.mark.parametrize("types,pair,A", [("1", "1", 200), ("3", "1", 200), ("3", "1", 300),
                                           ("3", "0", 200), ("5", "1", 200), ("15", "1", 200),
                                           ("110", "0", 200), ("106", "0", 300), ("105", "0", 200),
-                                          ("103", "0", 300), ("212", "0", 300), ("210", "0", 200),
-                                          ("206", "0", 300)])
+                                          ("103", "0", 300), ("206", "0", 300), ("206", "0", 200)])
 def test_factor_workgroup_splits_identical(types, pair, A, monkeypatch):
     """Every launch shape gives the same bit-exact panel and masks: the 15-set partition split
     over 1, 3, 5 or 15 workgroups per block (paired two items per workgroup or not, factor_pair;
     A = 300 leaves the last pair half idle), and the 30-set small-grid partition (split
     correlations, return rings) over 10, 6, 5 or 3 workgroups per block (codes 110 / 106 / 105 /
     103: 3, 5, 6, 10 job waves each), and the 60-set partition (split correlations and sd ratios)
-    over 12, 10 or 6 (codes 212 / 210 / 206: 5, 6, 10 job waves).  The shape is chosen from the
-    shard's block count; the context option factor_split overrides."""
+    over 6 workgroups of 10 job waves (code 206).  The shape is chosen from the shard's block
+    count; the context option factor_split overrides."""
     import torch
     import afm
     from afm.synthetic import make_panel

@@ -76,7 +76,7 @@ def test_group_sizing():
 
 
 @pytest.mark.parametrize("types,step", [(15, 64), (5, 320), (3, 1024), (3, 704), (110, 64),
-                                        (106, 320), (103, 704), (212, 64), (206, 704)])
+                                        (106, 320), (103, 704), (206, 64), (206, 704)])
 def test_time_slabs_identical_to_one_launch(monkeypatch, types, step):
     """Config D's default build: ALL assets over consecutive time slabs, every recurrence state
     and observation ring carried across slab boundaries in the state buffer -- the concatenated
