@@ -1,0 +1,28 @@
+#!/bin/bash
+# round 5: FM Grams (zgram NT = 2) with two MFMA accumulation chains per consumer (even / odd k-steps)
+# -- parity, then headline / emulated world-8 A/B against one chain (acc1)
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R; o=gpurun_out/r5x; mkdir -p $o
+timeout -k 10 900 python -u -m pytest tests/test_zgram_wide_gpu.py tests/test_regression_gpu.py tests/test_chain_gpu.py tests/test_sharded.py tests/test_configs_gpu.py -x -v -m gpu --timeout 400 --timeout-method thread > $o/tests.log 2>&1
+rc=$?; tail -3 $o/tests.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $o/tests.log | head -30; exit 1; }
+B=alpha-multi-factor-models_amd/build/exp
+show() { python3 -c "
+import json; d=json.loads(open('$1').read().strip().splitlines()[-1])
+print('$2', d['ms_per_step'], {k: round(v,2) for k,v in d.get('stage_ms',{}).items()})"; }
+for rep in 1 2; do
+  for v in default acc1; do
+    if [ $v = default ]; then lib=""; else lib=$R/$B/$v/libafm.so; fi
+    AFM_LIB=$lib timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-configs --no-variants > $o/$v.$rep.json 2> $o/$v.$rep.err || { echo "$v failed"; tail -5 $o/$v.$rep.err; exit 1; }
+    show $o/$v.$rep.json "$v $rep"
+    AFM_LIB=$lib timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --emulate-world 8 --no-cpu-baseline --no-configs --no-variants > $o/emu8_$v.$rep.json 2> $o/emu8_$v.$rep.err || { echo "emu8 $v failed"; tail -5 $o/emu8_$v.$rep.err; exit 1; }
+    show $o/emu8_$v.$rep.json "emu8 $v $rep"
+  done
+done
+cd /tmp && export TMPDIR=/tmp
+for v in default acc1; do
+  if [ $v = default ]; then lib=""; else lib=$R/$B/$v/libafm.so; fi
+  AFM_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r5x_$v -o run --output-format csv -- \
+      python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-configs --no-variants > $R/gpurun_out/r5x_$v.log 2>&1 || { echo "prof failed"; tail -20 $R/gpurun_out/r5x_$v.log; exit 1; }
+  python3 $R/tools/rocprof_summary.py $R/gpurun_out/r5x_$v/run_kernel_trace.csv > $R/gpurun_out/r5x_${v}_kernel_stats.txt
+  grep -E "zgram_kernel<2" $R/gpurun_out/r5x_${v}_kernel_stats.txt
+done
