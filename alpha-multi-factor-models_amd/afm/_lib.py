@@ -67,6 +67,8 @@ SIGNATURES = {
     "afm_xs_stats_f64": (I32, [P, I64, I64, P, I64, P, P, P, P, I32, P, P, P, P]),
     "afm_xs_series_f64": (I32, [P, I64, P, P, P, P, I32, I32, P, P, P, P, P]),
     "afm_zscore_stats_f64": (I32, [P, P, I64, I64, I64, P, I32, P, I64, I64, P, P]),
+    "afm_zscore_stats_slab_f64": (I32, [P, P, I64, I64, I64, P, I32, P, I64, I64, P, I32, I32,
+                                        P, P]),
     "afm_zscore_apply_f64": (I32, [P, P, I64, I64, I64, P, I32, P, I64, I64, P, P, P, I64, P, P]),
     "afm_zgram_part_bytes": (I32, [I32]),
     "afm_zstats_finalize_f64": (I32, [P, P, P, I32, I64, P, P]),

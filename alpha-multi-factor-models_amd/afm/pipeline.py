@@ -117,6 +117,12 @@ class PipelineConfig:
     # (1,280 assets): 8.97 ms per step either way -- the second slab is the ~17 % of dates after
     # the train window, and the z statistics beside it ran 1.69 instead of 1.03 ms -- so off
     early_zstats: bool = False
+    # zstats_slabs -- the factor panel in this many time slabs with the train window's z
+    # statistics streamed slab by slab on a side stream right behind them (the recurrences' state
+    # carried, afm_zscore_stats_slab_f64): on the smallest grids (the factor launch with one job
+    # wave per SIMD, <= 25 blocks: the N = 8 shard) the z statistics then run on the issue slots
+    # and CUs the factor kernel leaves free instead of after it.  -1: 6 on those grids, else 0.
+    zstats_slabs: int = -1
     # early_fwd -- one GPU: the analyzer's price rows and forward returns (prediction-independent,
     # KKT:294-296) on a side stream as soon as the all_df rows exist, beside the z statistics,
     # instead of at the head of the analyzer stream in the tail
@@ -381,12 +387,25 @@ class Pipeline:
         # early z statistics: the first slab ends at the first 64-date boundary past the train
         # window (the slab API's alignment)
         self.ta = min(((sp.tr1 + 63) // 64) * 64, T)
-        self.early = bool(c.early_zstats) and self.A_r > 0 and self.ta < T
-        if self.early:
+        nslab = c.zstats_slabs
+        if nslab < 0:
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            nslab = 6 if ((self.A_r + 63) // 64) * 10 <= ncu else 0
+        self.stream_z = nslab >= 2 and self.A_r > 0 and sp.tr1 > 0 and T >= 128
+        if self.stream_z:
+            bounds = sorted({0, T} | {min(T, ((i * T // nslab + 63) // 64) * 64)
+                                      for i in range(1, nslab)})
+            self.zbounds = bounds
+            self.zstate = torch.empty((5, p, lda_r), **f64)
+            self.zslab_done = [torch.cuda.Event() for _ in bounds[:-1]]
+            self.zstats_done = torch.cuda.Event()
+        self.early = (bool(c.early_zstats) and not self.stream_z and self.A_r > 0 and self.ta < T)
+        if self.early or self.stream_z:
             nb = int(L.afm_factors_state_bytes(self.ctx.handle, self.A_r))
             self.fstate = torch.empty(nb // 8 + 1, **f64)
             self.slab1_done = torch.cuda.Event()
-            self.zstats_done = torch.cuda.Event()
+            if not self.stream_z:
+                self.zstats_done = torch.cuda.Event()
 
     def n_asset_days_local(self) -> int:
         return int(self.g.valid.sum().item())
@@ -448,6 +467,58 @@ class Pipeline:
             chk(L.afm_ols_solve_f64(h, P(self.fm_gram), P(self.fm_shift), pf, self.fnd, c.tol,
                                     P(self.fm_beta_own), P(self.fm_nobs_own),
                                     P(self.fm_rank_own)), "fm solve")
+
+    def _factors_streamed(self, h, mark):
+        """The factor panel in time slabs (zbounds) on the main stream, each slab's all_df rows
+        right behind it, and the train window's z statistics streamed slab by slab on the side
+        stream as each slab lands (afm_zscore_stats_slab_f64, every (feature, asset) recurrence
+        carried): bitwise the panel, statistics and row sets of one call each.  The label planes
+        go first, once, on the second side stream (inputs only; tmr_ret1d is a feature) -- not
+        inside every factor slab."""
+        import torch
+        L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+        g, sp, T, lda_r, p, A_r = self.g, self.sp, self.T, self.lda_r, self.p, self.A_r
+        lab = (None, None)
+        with torch.cuda.stream(self.side2):
+            h2 = self.ctx.bind_stream()
+            chk(L.afm_labels_f64(h2, T, lda_r, 0, T, P(g.excess), P(g.ret1d), P(g.vbits),
+                                 P(self.out[TARGET]), P(self.out[TMR])), "labels")
+            self.labels_done.record(self.side2)
+        h = self.ctx.bind_stream()
+        b, tr1 = self.zbounds, sp.tr1
+        for i in range(len(b) - 1):
+            t0, t1 = b[i], b[i + 1]
+            chk(L.afm_factors_range_f64(h, T, A_r, lda_r, t0, t1, P(g.close), P(g.volume), *lab,
+                                        P(g.vbits), P(self.out), P(self.nanfree),
+                                        P(self.finite), P(self.fstate)), "factors slab")
+            for src, dst in ((self.nanfree, self.alldf), (self.finite, self.frows)):
+                chk(L.afm_drop_last_obs_bits_range(h, T, lda_r, P(g.vbits), P(src), P(dst), t0,
+                                                   t1), "last-obs rows")
+            if t0 < tr1:
+                self.zslab_done[i].record(self.main)
+                with torch.cuda.stream(self.side):
+                    hs = self.ctx.bind_stream()
+                    self.side.wait_event(self.zslab_done[i])
+                    if i == 0:
+                        self.side.wait_event(self.labels_done)
+                        mark("zstats", 0)
+                    last = t1 >= tr1
+                    chk(L.afm_zscore_stats_slab_f64(hs, P(self.out), T * lda_r, T, lda_r,
+                                                    P(self.feat), p, P(self.alldf), t0,
+                                                    min(t1, tr1), P(self.zstate), int(i == 0),
+                                                    int(last), P(self.mu), P(self.sd)),
+                        "zscore stats slab")
+                    if last:
+                        chk(L.afm_zstats_finalize_f64(hs, P(self.mu), P(self.sd), p, lda_r,
+                                                      P(self.zs), P(self.asset_ok)),
+                            "zstats finalize")
+                        mark("zstats", 1)
+                        self.zstats_done.record(self.side)
+                h = self.ctx.bind_stream()
+        mark("factors", 1)
+        self.main.wait_event(self.zstats_done)
+        chk(L.afm_row_bits(h, self.nch, lda_r, P(self.frows), None, P(self.asset_ok), 0, T,
+                           P(self.zrows)), "z rows")
 
     def _factors_early(self, h, lab_side, mark):
         """The factor panel in two slabs [0, ta) and [ta, T) on the main stream; the train
@@ -520,7 +591,10 @@ class Pipeline:
             # one GPU: the two label planes on the side stream, enqueued after the factor kernel
             # (it runs on the CUs the factor workgroups leave free); zstats waits for them
             lab_side = W == 1 and c.labels_side
-            if self.early:
+            if self.stream_z:
+                self._factors_streamed(h, mark)
+                h = self.ctx.bind_stream()
+            elif self.early:
                 self._factors_early(h, lab_side, mark)
                 h = self.ctx.bind_stream()
             elif self.A_r > 0:
@@ -540,7 +614,8 @@ class Pipeline:
                                              P(self.alldf)), "all_df rows")
                 chk(L.afm_drop_last_obs_bits(h, T, lda_r, P(g.vbits), P(self.finite),
                                              P(self.frows)), "finite rows")
-            if not self.early:
+            one_pass = not (self.early or self.stream_z)
+            if one_pass:
                 mark("factors", 1)
             self.fwd_early = W == 1 and c.analyzer and c.early_fwd
             if self.fwd_early:
@@ -548,9 +623,9 @@ class Pipeline:
                 with torch.cuda.stream(self.side2):
                     self._analyzer_fwd()
                 h = self.ctx.bind_stream()
-            if not self.early:
+            if one_pass:
                 mark("zstats", 0)
-            if self.A_r > 0 and not self.early:
+            if self.A_r > 0 and one_pass:
                 if lab_side:
                     self.main.wait_event(self.labels_done)          # tmr_ret1d is a feature
                 chk(L.afm_zscore_stats_f64(h, P(self.out), T * lda_r, T, lda_r, P(self.feat), p,
@@ -560,7 +635,8 @@ class Pipeline:
                                               P(self.asset_ok)), "zstats finalize")
                 chk(L.afm_row_bits(h, nch, lda_r, P(self.frows), None, P(self.asset_ok), 0, T,
                                    P(self.zrows)), "z rows")
-            mark("zstats", 1)
+            if one_pass:
+                mark("zstats", 1)
             if W > 1:           # full-width label planes for the rebalance, during the Grams
                 with torch.cuda.stream(self.side2):
                     h2 = self.ctx.bind_stream()

@@ -107,6 +107,75 @@ __global__ __launch_bounds__(NT) void zscore_stats_kernel(const double* base, in
     sd[(int64_t)k * lda + a] = nobs <= 1 ? qnan() : __builtin_sqrt(m2 / (ct - 1.0));
 }
 
+// Streamed z statistics (round 5; the smallest grids, beside the factor kernel's time slabs): the
+// same recurrences over the dates [t0, t1) of one slab, each (column, asset) state -- Kahan sum and
+// compensation, Welford mean and M2, the count -- carried in st [6][K][lda] between slabs (first:
+// start from zero; last: write mu / sd, else store the state).  The Welford quotient is the IEEE
+// division (the value the reciprocal table's Markstein step reproduces), so the kernel needs no
+// LDS and its waves fit beside a factor workgroup that holds 140 KB of a CU.  Bitwise the
+// statistics of one zscore_stats_kernel pass over the union of the slabs.
+__global__ __launch_bounds__(256) void zscore_stats_slab_kernel(const double* base,
+                                                                int64_t col_stride, int64_t lda,
+                                                                const int32_t* cols, int K,
+                                                                const uint64_t* bits, int64_t t0,
+                                                                int64_t t1, double* st, int first,
+                                                                int last, double* mu, double* sd) {
+    const int64_t a = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int k = blockIdx.y;
+    if (a >= lda) return;
+    const double* x = base + (int64_t)cols[k] * col_stride + a;
+    const int64_t sl = (int64_t)K * lda, si = (int64_t)k * lda + a;
+    double sum = 0.0, comp = 0.0, mean = 0.0, m2 = 0.0;
+    int nobs = 0;
+    if (!first) {
+        sum = st[si];
+        comp = st[sl + si];
+        mean = st[2 * sl + si];
+        m2 = st[3 * sl + si];
+        nobs = (int)st[4 * sl + si];
+    }
+    for (int64_t c = t0 >> 6; c <= (t1 - 1) >> 6; ++c) {
+        u64 w = bits[c * lda + a];
+        const int64_t d0 = c << 6;
+        if (d0 < t0) w &= ~0ull << (t0 - d0);
+        if (t1 - d0 < 64) w &= (1ull << (t1 - d0)) - 1ull;
+        for (int j0 = 0; j0 < 64; j0 += kUnroll) {
+            const u64 wb = (w >> j0) & ((1ull << kUnroll) - 1ull);
+            if (!__any(wb != 0)) continue;
+            double v[kUnroll];
+#pragma unroll
+            for (int j = 0; j < kUnroll; ++j)
+                v[j] = ((wb >> j) & 1ull) ? x[(d0 + j0 + j) * lda] : qnan();
+#pragma unroll
+            for (int j = 0; j < kUnroll; ++j) {
+                const double val = v[j];
+                if (val == val) {                       // absent rows read NaN: skipped
+                    nobs += 1;
+                    const double y = val - comp;
+                    const double t = sum + y;
+                    comp = t - sum - y;
+                    if (comp != comp) comp = 0.0;
+                    sum = t;
+                    const double old = mean;
+                    mean = mean + (val - old) / (double)nobs;
+                    m2 = m2 + (val - mean) * (val - old);
+                }
+            }
+        }
+    }
+    if (last) {
+        const double ct = (double)nobs;
+        mu[si] = nobs == 0 ? qnan() : sum / ct;
+        sd[si] = nobs <= 1 ? qnan() : __builtin_sqrt(m2 / (ct - 1.0));
+    } else {
+        st[si] = sum;
+        st[sl + si] = comp;
+        st[2 * sl + si] = mean;
+        st[3 * sl + si] = m2;
+        st[4 * sl + si] = (double)nobs;
+    }
+}
+
 // grid (ceil(lda / 256), chunks of [t0, t1)); thread = (asset a, chunk c)
 __global__ __launch_bounds__(256) void zscore_apply_kernel(const double* base, int64_t col_stride,
                                                            int64_t lda, const int32_t* cols, int K,
@@ -188,6 +257,23 @@ extern "C" int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t co
         hipLaunchKernelGGL((zscore_stats_kernel<256, false>), grid, dim3(256), 0, ctx->stream,
                            base, col_stride, lda, cols, bits, t0, t1, mu, sd);
     }
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int afm_zscore_stats_slab_f64(afm_ctx* ctx, const double* base, int64_t col_stride,
+                                         int64_t T, int64_t lda, const int32_t* cols, int K,
+                                         const uint64_t* bits, int64_t t0, int64_t t1,
+                                         double* state, int first, int last, double* mu,
+                                         double* sd) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(base && cols && bits && state && (!last || (mu && sd)), "null buffer");
+    AFM_CHECK_ARG(lda > 0 && lda % 64 == 0 && K >= 1 && K <= 65535, "bad shape");
+    AFM_CHECK_ARG(col_stride >= T * lda, "col_stride smaller than a [T][lda] plane");
+    AFM_CHECK_ARG(0 <= t0 && t0 < t1 && t1 <= T, "bad date range (a slab holds at least one date)");
+    dim3 grid((unsigned)((lda + 255) / 256), (unsigned)K);
+    hipLaunchKernelGGL(zscore_stats_slab_kernel, grid, dim3(256), 0, ctx->stream, base, col_stride,
+                       lda, cols, K, bits, t0, t1, state, first, last, mu, sd);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

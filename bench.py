@@ -345,6 +345,8 @@ def main():
                     help="PipelineConfig.fm_free_cus (CUs the FM side stream leaves free)")
     ap.add_argument("--fm-fork", default=None,
                     help="PipelineConfig.fm_fork (where the FM Grams fork off the main stream)")
+    ap.add_argument("--zstats-slabs", type=int, default=None,
+                    help="PipelineConfig.zstats_slabs (A/B; default: the pipeline's auto rule)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="time what ONE rank of an N-GPU job computes, on one GPU (collectives "
                          "replaced by local copies, afm.sharded.EmulatedComm): a per-rank proxy, "
@@ -397,6 +399,8 @@ def main():
         place["fm_free_cus"] = args.fm_free_cus
     if args.fm_fork is not None:
         place["fm_fork"] = args.fm_fork
+    if args.zstats_slabs is not None:
+        place["zstats_slabs"] = args.zstats_slabs
     cfg = PipelineConfig(top_n=args.top_n, **place)
     if world > 1:
         from afm.sharded import EXCHANGE_STAGES, Comm, ShardedPipeline

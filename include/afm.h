@@ -296,6 +296,14 @@ int afm_xs_series_f64(afm_ctx* ctx, int64_t nd, const double* layer_mean, const 
 int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t T,
                          int64_t lda, const int32_t* cols, int K, const uint64_t* bits,
                          int64_t t0, int64_t t1, double* mu, double* sd);
+/* The same statistics streamed over consecutive date slabs [t0, t1) of one series (each slab at
+ * least one date, the slabs in order): state [6][K][lda] doubles carries every (column, asset)
+ * recurrence between the calls; first != 0 starts from zero, last != 0 writes mu / sd (else the
+ * state is stored).  Bitwise the statistics of one afm_zscore_stats_f64 call over the union. */
+int afm_zscore_stats_slab_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t T,
+                              int64_t lda, const int32_t* cols, int K, const uint64_t* bits,
+                              int64_t t0, int64_t t1, double* state, int first, int last,
+                              double* mu, double* sd);
 /* Over the rows of [t0, t1): z = (x - mu) / sd (IEEE), +-inf -> NaN, written to the plane
  * out + out_cols[k] * out_col_stride (out may alias base: in place when out_cols == cols);
  * other cells are not written.  keep [ceil(T/64)][lda]: the row bits of [t0, t1) with every z

@@ -131,13 +131,16 @@ def test_fama_macbeth_vs_golden(chain_a):
 
 @pytest.mark.parametrize("place", [{"labels_side": False}, {"fm_fork": "gram"},
                                    {"fm_fork": "rebalance"}, {"fm_free_cus": 8},
-                                   {"early_zstats": True},
-                                   {"early_zstats": True, "labels_side": False},
-                                   {"early_fwd": False}])
+                                   {"early_zstats": True, "zstats_slabs": 0},
+                                   {"early_zstats": True, "labels_side": False, "zstats_slabs": 0},
+                                   {"early_fwd": False}, {"zstats_slabs": 0},
+                                   {"zstats_slabs": 3}, {"zstats_slabs": 6, "labels_side": False}])
 def test_stream_placement_bit_identical(chain_a, place):
     """The side-stream placements (label planes beside the factor kernel, the FM fork point) move
     work between streams only: the step's outputs are bitwise those of the default placement.
-    early_zstats builds the panel in two time slabs with the z statistics between them."""
+    early_zstats builds the panel in two time slabs with the z statistics between them;
+    zstats_slabs streams the z statistics slab by slab behind the factor slabs (the default on
+    this 500-asset grid: the reference step runs it, zstats_slabs = 0 is the one-pass path)."""
     import torch
     from afm.pipeline import Pipeline, PipelineConfig
     p, pipe, gold, C = chain_a
@@ -145,8 +148,13 @@ def test_stream_placement_bit_identical(chain_a, place):
                                             window=C["window"], top_n=C["top_n"], **place))
     other.step()
     torch.cuda.synchronize()
+    assert pipe.stream_z                              # the auto rule on a 500-asset grid
     if place.get("early_zstats"):
         assert other.early and 0 < other.ta < other.T
+    if place.get("zstats_slabs", -1) >= 2:
+        assert other.stream_z and len(other.zbounds) - 1 == place["zstats_slabs"]
+    if place.get("zstats_slabs", -1) == 0:
+        assert not other.stream_z
     for name in ("out", "pred", "lasso_beta", "fm_beta", "zs", "nanfree", "finite", "alldf",
                  "frows", "zrows", "pool_g"):
         a, b = getattr(pipe, name), getattr(other, name)
