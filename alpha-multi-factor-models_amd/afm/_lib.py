@@ -43,6 +43,9 @@ SIGNATURES = {
     "afm_labels_f64": (I32, [P, I64, I64, I64, I64, P, P, P, P, P]),
     "afm_drop_last_obs_bits": (I32, [P, I64, I64, P, P, P]),
     "afm_drop_last_obs_bits_range": (I32, [P, I64, I64, P, P, P, I64, I64]),
+    "afm_factors_part_words": (I64, [P, I64, I64, I64, I64]),
+    "afm_factors_range_part_f64": (I32, [P, I64, I64, I64, I64, I64, P, P, P, P, P, P]),
+    "afm_factor_masks_f64": (I32, [P, I64, I64, I64, I64, I64, P, P, P, P]),
     "afm_predict_f64": (I32, [P, P, I64, I64, I64, I64, P, I32, P, I64, P, I32, P]),
     "afm_fama_macbeth_f64": (I32, [P, P, P, I64, I32, P, P]),
     "afm_ols_residual_f64": (I32, [P, P, I64, I32, I32, P, P, P]),

@@ -397,6 +397,9 @@ class Pipeline:
                                       for i in range(1, nslab)})
             self.zbounds = bounds
             self.zstate = torch.empty((5, p, lda_r), **f64)
+            self.zparts = [torch.empty(int(L.afm_factors_part_words(self.ctx.handle, self.A_r,
+                                                                    lda_r, a, z)), **i64)
+                           for a, z in zip(bounds[:-1], bounds[1:])]
             self.zslab_done = [torch.cuda.Event() for _ in bounds[:-1]]
             self.zstats_done = torch.cuda.Event()
         self.early = (bool(c.early_zstats) and not self.stream_z and self.A_r > 0 and self.ta < T)
@@ -478,7 +481,6 @@ class Pipeline:
         import torch
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
         g, sp, T, lda_r, p, A_r = self.g, self.sp, self.T, self.lda_r, self.p, self.A_r
-        lab = (None, None)
         with torch.cuda.stream(self.side2):
             h2 = self.ctx.bind_stream()
             chk(L.afm_labels_f64(h2, T, lda_r, 0, T, P(g.excess), P(g.ret1d), P(g.vbits),
@@ -488,17 +490,25 @@ class Pipeline:
         b, tr1 = self.zbounds, sp.tr1
         for i in range(len(b) - 1):
             t0, t1 = b[i], b[i + 1]
-            chk(L.afm_factors_range_f64(h, T, A_r, lda_r, t0, t1, P(g.close), P(g.volume), *lab,
-                                        P(g.vbits), P(self.out), P(self.nanfree),
-                                        P(self.finite), P(self.fstate)), "factors slab")
-            for src, dst in ((self.nanfree, self.alldf), (self.finite, self.frows)):
-                chk(L.afm_drop_last_obs_bits_range(h, T, lda_r, P(g.vbits), P(src), P(dst), t0,
-                                                   t1), "last-obs rows")
-            if t0 < tr1:
-                self.zslab_done[i].record(self.main)
-                with torch.cuda.stream(self.side):
-                    hs = self.ctx.bind_stream()
-                    self.side.wait_event(self.zslab_done[i])
+            # the slab on the main stream; its row masks, all_df rows and z statistics on the side
+            # stream beside the next slab (the next slab needs only the carried factor state)
+            need = int(L.afm_factors_part_words(self.ctx.handle, A_r, lda_r, t0, t1))
+            if need > self.zparts[i].numel():    # (an execution option changed the launch shape)
+                self.zparts[i] = torch.empty(need, dtype=torch.int64, device=self.out.device)
+            part = self.zparts[i]
+            chk(L.afm_factors_range_part_f64(h, T, A_r, lda_r, t0, t1, P(g.close), P(g.volume),
+                                             P(g.vbits), P(self.out), P(self.fstate), P(part)),
+                "factors slab")
+            self.zslab_done[i].record(self.main)
+            with torch.cuda.stream(self.side):
+                hs = self.ctx.bind_stream()
+                self.side.wait_event(self.zslab_done[i])
+                chk(L.afm_factor_masks_f64(hs, T, A_r, lda_r, t0, t1, P(g.vbits), P(part),
+                                           P(self.nanfree), P(self.finite)), "factor masks")
+                for src, dst in ((self.nanfree, self.alldf), (self.finite, self.frows)):
+                    chk(L.afm_drop_last_obs_bits_range(hs, T, lda_r, P(g.vbits), P(src), P(dst),
+                                                       t0, t1), "last-obs rows")
+                if t0 < tr1:
                     if i == 0:
                         self.side.wait_event(self.labels_done)
                         mark("zstats", 0)
@@ -513,9 +523,9 @@ class Pipeline:
                                                       P(self.zs), P(self.asset_ok)),
                             "zstats finalize")
                         mark("zstats", 1)
-                        self.zstats_done.record(self.side)
-                h = self.ctx.bind_stream()
+            h = self.ctx.bind_stream()
         mark("factors", 1)
+        self.zstats_done.record(self.side)        # every slab's masks, rows and statistics
         self.main.wait_event(self.zstats_done)
         chk(L.afm_row_bits(h, self.nch, lda_r, P(self.frows), None, P(self.asset_ok), 0, T,
                            P(self.zrows)), "z rows")

@@ -2282,7 +2282,9 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
                         const double* close, const double* volume, const double* ret1d,
                         const double* excess, const uint64_t* valid_bits, double* out,
                         uint64_t* nanfree_bits, uint64_t* finite_bits, double* state,
-                        bool full = false) {
+                        bool full = false, uint64_t* ext_part = nullptr) {
+    // ext_part: the caller's buffer for the mask partials (afm_factors_part_words); the masks
+    // are then left to afm_factor_masks_f64
     // full: out / nanfree / finite are the whole [T]-date panel and bit words (the slab's rows
     // and words written in place); else they hold the slab's dates only
     const int64_t nwords = (t1 - t0 + 63) / 64;                   // the slab's mask words
@@ -2312,9 +2314,10 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     const int64_t nblk = (A + 63) / 64;
     const int code = factor_types(ctx, nblk);
     const int types = code_types(code), nparts = code_parts(code);
-    uint64_t* part = nullptr;         // per-job-wave mask partials (masks_kernel ORs them)
-    AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * nparts * nwords * lda,
-                           ctx->stream));
+    uint64_t* part = ext_part;        // per-job-wave mask partials (masks_kernel ORs them)
+    if (!ext_part)
+        AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * nparts * nwords * lda,
+                               ctx->stream));
     afm::Args a;
     a.T = T;
     a.lda = lda;
@@ -2362,10 +2365,11 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
             rc = AFM_E_ARG;
     }
     if (rc != AFM_OK) {
-        (void)hipFreeAsync(part, ctx->stream);
+        if (!ext_part) (void)hipFreeAsync(part, ctx->stream);
         return rc;
     }
     AFM_HIP(hipGetLastError());
+    if (ext_part) return AFM_OK;      // (labels: this entry takes none, see the header)
     const int64_t nw = nwords * lda;
     // columns past A (lda padding) carry no presence: their mask words come from valid_bits
     // (zero there), and the factor kernel never ran on blocks past ceil(A/64)
@@ -2485,6 +2489,48 @@ extern "C" int afm_drop_last_obs_bits_range(afm_ctx* ctx, int64_t T, int64_t lda
     hipLaunchKernelGGL(afm::drop_last_obs_kernel, dim3((unsigned)((lda + 255) / 256)), dim3(256),
                        0, ctx->stream, (T + 63) / 64, lda, valid_bits, in_bits, out_bits,
                        t0 / 64, (t1 + 63) / 64);
+    AFM_HIP(hipGetLastError());
+    return AFM_OK;
+}
+
+extern "C" int64_t afm_factors_part_words(afm_ctx* ctx, int64_t A, int64_t lda, int64_t t0,
+                                          int64_t t1) {
+    if (!ctx || A <= 0 || lda < A || t1 <= t0) return -1;
+    const int code = factor_types(ctx, (A + 63) / 64);
+    return 2 * (int64_t)code_parts(code) * ((t1 - t0 + 63) / 64) * lda;
+}
+
+extern "C" int afm_factors_range_part_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda,
+                                          int64_t t0, int64_t t1, const double* close,
+                                          const double* volume, const uint64_t* valid_bits,
+                                          double* out, double* state, uint64_t* part) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && A > 0, "T and A must be positive");
+    AFM_CHECK_ARG(lda >= A && lda % 64 == 0, "lda must be a multiple of 64 and >= A");
+    AFM_CHECK_ARG(close && volume && valid_bits && out && state && part, "null buffer");
+    AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
+    AFM_CHECK_ARG(0 <= t0 && t0 < t1 && t1 <= T && t0 % 64 == 0 && (t1 % 64 == 0 || t1 == T),
+                  "need 0 <= t0 < t1 <= T with t0 and t1 (unless T) multiples of 64");
+    // (the bit-word pointers are not written on this path: the masks come later)
+    uint64_t dummy = 0;
+    return factors_slab(ctx, T, A, lda, t0, t1, close, volume, nullptr, nullptr, valid_bits, out,
+                        &dummy, nullptr, state, true, part);
+}
+
+extern "C" int afm_factor_masks_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,
+                                    int64_t t1, const uint64_t* valid_bits, const uint64_t* part,
+                                    uint64_t* nanfree_bits, uint64_t* finite_bits) {
+    AFM_CTX(ctx);
+    AFM_CHECK_ARG(T > 0 && A > 0 && lda >= A && lda % 64 == 0, "bad shape");
+    AFM_CHECK_ARG(valid_bits && part && nanfree_bits, "null buffer");
+    AFM_CHECK_ARG(0 <= t0 && t0 < t1 && t1 <= T && t0 % 64 == 0, "bad date range");
+    const int code = factor_types(ctx, (A + 63) / 64);
+    const int64_t nwords = (t1 - t0 + 63) / 64, nw = nwords * lda;
+    const int nparts = code_parts(code);
+    hipLaunchKernelGGL(afm::masks_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0,
+                       ctx->stream, nwords, lda, nparts, valid_bits + (t0 / 64) * lda, part,
+                       part + nparts * nw, nanfree_bits + (t0 / 64) * lda,
+                       finite_bits ? finite_bits + (t0 / 64) * lda : nullptr);
     AFM_HIP(hipGetLastError());
     return AFM_OK;
 }

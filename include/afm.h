@@ -102,6 +102,21 @@ int afm_factors_range_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64
                           double* out, uint64_t* nanfree_bits, uint64_t* finite_bits,
                           double* state);
 
+/* afm_factors_range_f64 with the row masks left to the caller (no label planes): the factor
+ * kernel's per-job-wave NaN / non-finite partial words go to part (afm_factors_part_words(ctx, A,
+ * lda, t0, t1) uint64 words), and afm_factor_masks_f64 ORs them into the whole-panel
+ * nanfree_bits / finite_bits words of [t0, t1) -- on any stream ordered after the slab, so a
+ * pipeline runs the masks and what reads them beside the next slab.  The same execution options
+ * (factor_split) for both calls. */
+int64_t afm_factors_part_words(afm_ctx* ctx, int64_t A, int64_t lda, int64_t t0, int64_t t1);
+int afm_factors_range_part_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,
+                               int64_t t1, const double* close, const double* volume,
+                               const uint64_t* valid_bits, double* out, double* state,
+                               uint64_t* part);
+int afm_factor_masks_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0, int64_t t1,
+                         const uint64_t* valid_bits, const uint64_t* part, uint64_t* nanfree_bits,
+                         uint64_t* finite_bits);
+
 /* out_bits = in_bits without each asset's last present day (valid_bits): the rows whose
  * shift(-1) labels are NaN.  Used to mask the regression rows up front (the Gram's REDO pass
  * would otherwise re-run those dates). */

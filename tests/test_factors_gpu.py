@@ -139,3 +139,36 @@ def test_clean_fast_step_matches_general_step(monkeypatch, split):
     tt, aa, ref = oracle_panel(p)
     got = b[:, torch.from_numpy(tt).cuda(), torch.from_numpy(aa).cuda()].T.cpu().numpy()
     assert same(got, ref), mismatch_report(got, ref, afm.FACTOR_NAMES)
+
+
+@pytest.mark.parametrize("split", [0, 110, 3])
+def test_factor_range_part_and_masks_identical(split):
+    """afm_factors_range_part_f64 (mask partials to a caller buffer, no labels) slab by slab with
+    afm_factor_masks_f64 run afterwards equals one afm_factors_f64 call: panel columns 0-95 and
+    both row masks, bit for bit."""
+    import torch
+    import afm
+    from afm import _lib
+    from afm.synthetic import make_panel
+    L, P, chk = _lib.lib(), _lib.ptr, _lib.check
+    p = make_panel(300, 450, seed=21, edge_cases=True, hole_frac=0.01, listing_frac=0.2)
+    grid = afm.PanelGrid.from_panel(p)
+    with _lib.options(factor_split=split) as ctx:
+        fin = torch.zeros_like(grid.vbits)
+        out, nanfree = afm.factor_panel(grid, finite=fin)
+        T, A, lda = p.T, p.A, grid.lda
+        h = ctx.bind_stream()
+        out2 = torch.full_like(out, float("nan"))
+        nf2, fin2 = torch.zeros_like(nanfree), torch.zeros_like(fin)
+        st = torch.empty(int(L.afm_factors_state_bytes(ctx.handle, A)) // 8 + 1,
+                         dtype=torch.float64, device="cuda")
+        for t0, t1 in ((0, 128), (128, 320), (320, T)):
+            part = torch.empty(int(L.afm_factors_part_words(ctx.handle, A, lda, t0, t1)),
+                               dtype=torch.int64, device="cuda")
+            chk(L.afm_factors_range_part_f64(h, T, A, lda, t0, t1, P(grid.close), P(grid.volume),
+                                             P(grid.vbits), P(out2), P(st), P(part)), "slab")
+            chk(L.afm_factor_masks_f64(h, T, A, lda, t0, t1, P(grid.vbits), P(part), P(nf2),
+                                       P(fin2)), "masks")
+        torch.cuda.synchronize()
+    assert torch.equal(out[:96].view(torch.int64), out2[:96].view(torch.int64))
+    assert torch.equal(nanfree, nf2) and torch.equal(fin, fin2)
