@@ -109,7 +109,7 @@ __global__ __launch_bounds__(NT) void zscore_stats_kernel(const double* base, in
 
 // Streamed z statistics (round 5; the smallest grids, beside the factor kernel's time slabs): the
 // same recurrences over the dates [t0, t1) of one slab, each (column, asset) state -- Kahan sum and
-// compensation, Welford mean and M2, the count -- carried in st [6][K][lda] between slabs (first:
+// compensation, Welford mean and M2, the count -- carried in st [5][K][lda] between slabs (first:
 // start from zero; last: write mu / sd, else store the state).  The Welford quotient is the IEEE
 // division (the value the reciprocal table's Markstein step reproduces), so the kernel needs no
 // LDS and its waves fit beside a factor workgroup that holds 140 KB of a CU.  Bitwise the

@@ -312,7 +312,7 @@ int afm_zscore_stats_f64(afm_ctx* ctx, const double* base, int64_t col_stride, i
                          int64_t lda, const int32_t* cols, int K, const uint64_t* bits,
                          int64_t t0, int64_t t1, double* mu, double* sd);
 /* The same statistics streamed over consecutive date slabs [t0, t1) of one series (each slab at
- * least one date, the slabs in order): state [6][K][lda] doubles carries every (column, asset)
+ * least one date, the slabs in order): state [5][K][lda] doubles carries every (column, asset)
  * recurrence between the calls; first != 0 starts from zero, last != 0 writes mu / sd (else the
  * state is stored).  Bitwise the statistics of one afm_zscore_stats_f64 call over the union. */
 int afm_zscore_stats_slab_f64(afm_ctx* ctx, const double* base, int64_t col_stride, int64_t T,
