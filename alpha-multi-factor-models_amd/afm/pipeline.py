@@ -111,6 +111,8 @@ class PipelineConfig:
     # stream, afm_stream_create_cu_mask), so the latency-bound tail beside the FM MFMA Grams keeps
     # whole CUs; 0 = an ordinary stream
     fm_free_cus: int = 0
+    # fm_grid -- the FM per-date Grams' persistent workgroups (0: one per CU); an A/B knob
+    fm_grid: int = 0
     # early_zstats -- the factor panel in two time slabs (afm_factors_range_f64): the train
     # window's z statistics run on a side stream while the second slab builds (a shard's factor
     # kernel leaves most of the GPU free: one wave per job set).  Measured at the N = 8 shard
@@ -372,7 +374,7 @@ class Pipeline:
             raise ValueError(f"fm_fork={c.fm_fork!r}: expected gram, predict, analyzer or "
                              "rebalance")
         self.main = torch.cuda.Stream(device=dev, priority=-8 if c.main_priority else 0)
-        self.fm_grid = 0                  # the FM Grams' persistent grid (0: one per CU)
+        self.fm_grid = c.fm_grid          # the FM Grams' persistent grid (0: one per CU)
         if c.fm_free_cus > 0:
             self._side_owner = _lib.cu_mask_stream(dev.index, c.fm_free_cus)
             self.side = self._side_owner.stream

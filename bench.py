@@ -345,6 +345,8 @@ def main():
                     help="PipelineConfig.fm_free_cus (CUs the FM side stream leaves free)")
     ap.add_argument("--fm-fork", default=None,
                     help="PipelineConfig.fm_fork (where the FM Grams fork off the main stream)")
+    ap.add_argument("--fm-grid", type=int, default=None,
+                    help="PipelineConfig.fm_grid (A/B; default: one FM workgroup per CU)")
     ap.add_argument("--zstats-slabs", type=int, default=None,
                     help="PipelineConfig.zstats_slabs (A/B; default: the pipeline's auto rule)")
     ap.add_argument("--emulate-world", type=int, default=0,
@@ -401,6 +403,8 @@ def main():
         place["fm_fork"] = args.fm_fork
     if args.zstats_slabs is not None:
         place["zstats_slabs"] = args.zstats_slabs
+    if args.fm_grid is not None:
+        place["fm_grid"] = args.fm_grid
     cfg = PipelineConfig(top_n=args.top_n, **place)
     if world > 1:
         from afm.sharded import EXCHANGE_STAGES, Comm, ShardedPipeline
