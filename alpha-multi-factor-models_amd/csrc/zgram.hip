@@ -43,6 +43,9 @@ constexpr int kZMaxSlots = 3;                // ring depth (2 when p + 4 staged 
 constexpr int kZLds = 160 * 1024 - 256;      // dynamic LDS budget of the ring
 constexpr int kZProd = 8;                    // producer waves
 constexpr int kZThreads = 13 * 64;           // 8 producers + up to 4 consumers + border wave
+#ifndef AFM_ZG2_NCW                          // (A/B builds: tools/build_flags_variant.sh)
+#define AFM_ZG2_NCW 3
+#endif
 
 // Shapes: NT 16-wide tiles (NT = 7: p + 2 <= 108, the 97-feature design; NT = 2: p + 2 <= 32,
 // the FM30 design).  Consumer wave c owns tile pairs [c * PPW, (c + 1) * PPW) of the J-major
@@ -51,7 +54,7 @@ template <int NT>
 struct ZCfg {
     static constexpr int NP = NT * (NT + 1) / 2;
     static constexpr int PE = NP * 256;                        // doubles of one partial
-    static constexpr int NCW = NT == 7 ? 4 : 3;                // consumer waves
+    static constexpr int NCW = NT == 7 ? 4 : AFM_ZG2_NCW;      // consumer waves
     // NT = 7: the columns of the last tile (96 .. p+1, at most 12) go to the border wave's VALU
     // sums; the MFMA consumers take the 21 pairs of tiles 0..5 -- 3 on wave 0 (which shares SIMD 0
     // with the border wave), 6 on each of waves 1..3.  NT = 2: all 3 pairs, one per wave.
@@ -576,7 +579,7 @@ __global__ __launch_bounds__(kZThreads, 1) void zgram_kernel(ZGramArgs g, int ns
     } else if (wave == 1) {
         zgram_consume<NT, 1>(g, sm, lane);
     } else if (wave == 2) {
-        zgram_consume<NT, 2>(g, sm, lane);
+        if constexpr (ZCfg<NT>::NCW >= 3) zgram_consume<NT, 2>(g, sm, lane);
     } else if constexpr (ZCfg<NT>::NCW == 4) {
         zgram_consume<NT, 3>(g, sm, lane);
     }
