@@ -11,10 +11,10 @@
 // One wave (after a block-wide setup of Q): lane j owns features j and j + 64 (p <= 110); H, w
 // and q live in registers; coordinates that cannot move are skipped by ballot (a sweep costs its
 // movable coordinates, not p); the Gram
-// Q sits in LDS (a row per coordinate, conflict-free); the scalar step of a coordinate is
-// computed redundantly by every lane from readlane broadcasts.  The work is a few hundred
-// flops per coordinate on a dependency chain: latency-bound by construction (one date-free
-// solve per fit, ~microseconds per sweep over 96 coordinates).
+// Q sits in LDS (a row per coordinate, conflict-free); a coordinate's step runs on its half's
+// registers in every lane of that half (lane c's result kept, then broadcast to the axpys).  The
+// work is a few hundred flops per coordinate on one in-order wave: its instruction count and
+// dependency chain bound it (one date-free solve per fit, ~microseconds per sweep).
 #include "afm_internal.h"
 
 #pragma clang fp contract(off)
@@ -38,19 +38,14 @@ __device__ __forceinline__ double pick(double v0, double v1, int j) {
     return j < 64 ? a : b;
 }
 __device__ __forceinline__ double fsign(double f) { return f == 0.0 ? 0.0 : (f > 0.0 ? 1.0 : -1.0); }
-// x / d with r = RN(1 / d): Markstein's correction q0 = RN(x r), e = fma(-q0, d, x),
+// computed here: an empty volatile asm on the value keeps the compiler from sinking its
+// producer into a later branch or behind a longer chain
+__device__ __forceinline__ void pin(double& v) { __asm__ volatile("" : "+v"(v)); }
+// The quotient x / d with r = RN(1 / d) by Markstein's correction q0 = RN(x r), e = fma(-q0, d, x),
 // q = RN(q0 + e r) is the IEEE quotient when r is the correctly rounded reciprocal and nothing
 // under- or overflows (checked on 5.6e8 hard and random cases, tools/markstein_any.c).  A zero x
 // gives x itself (d > 0: the signed zero the division would give); a quotient outside
-// [2^-400, 2^400] takes the IEEE division (a uniform branch, never in practice).
-__device__ __forceinline__ double div_r(double x, double d, double r) {
-    const double q0 = x * r;
-    const double e = __builtin_fma(-q0, d, x);
-    const double q1 = __builtin_fma(e, r, q0);
-    const double aq = __builtin_fabs(q0);
-    if (__builtin_expect(!(aq > 0x1p-400 && aq < 0x1p400), 0)) return x == 0.0 ? x : x / d;
-    return q1;
-}
+// [2^-400, 2^400] takes the IEEE division (a uniform branch, never in practice).  (`solve` below.)
 
 // alpha_row >= 0: alpha = alpha_row * n (sklearn's alpha times the row count, read on the device);
 // shift / beta_out (optional): beta_out = [intercept, w] with sklearn's _set_intercept,
@@ -101,80 +96,100 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     if (!(__builtin_fabs(rd1) > 0x1p-400 && __builtin_fabs(rd1) < 0x1p400)) rd1 = 0.0;
     // lanes whose coordinate exists and can ever move (a zero diagonal never moves)
     const uint64_t live0 = __ballot(has0 && qd0 != 0.0), live1 = __ballot(has1 && qd1 != 0.0);
-    // movable now (with its nonzero diagonal): w != 0, or the soft threshold of q - h is nonzero
-    // -- fmax(|t| - alpha, 0) != 0 is |t| > alpha (t - alpha = 0 only at t = alpha; NaN: false)
-    // (two ballots of plain compares: the lane masks go straight to SGPRs)
-    auto moves = [&](double q, double h, double w) -> uint64_t {
-        const double tmp = q - h;
-        return __builtin_amdgcn_ballot_w64(w != 0.0) |
-               __builtin_amdgcn_ballot_w64(POS ? tmp > alpha : __builtin_fabs(tmp) > alpha);
+    // the wave's largest of a non-negative per-lane double (fmax: order-free, NaN-ignoring)
+    auto wave_max = [](double v) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v = __builtin_fmax(v, __shfl_xor(v, o, 64));
+        return v;
     };
-    // the signed zero the skipped coordinate would store: fsign(tmp) * 0 / (qii + beta)
-    auto zero_of = [&](double q, double h) {
-        const double tmp = q - h;
-        return (POS && tmp < 0) ? 0.0 : (tmp < 0 ? -0.0 : 0.0);
-    };
-    // per-coordinate constants (q_j = X'y, the diagonal, its reciprocal) in LDS: the step reads
-    // them as broadcast loads beside the row instead of v_readlane picks
-    __shared__ double cq[kMaxLassoP], cqd[kMaxLassoP], crd[kMaxLassoP];
-    if (has0) { cq[j0] = q0; cqd[j0] = qd0; crd[j0] = rd0; }
-    if (has1) { cq[j1] = q1; cqd[j1] = qd1; crd[j1] = rd1; }
-    // lanes [lo, hi) of a half (lo, hi in 0..64) as a mask
-    auto span = [](int lo, int hi) -> uint64_t {
-        lo = lo < 0 ? 0 : (lo > 64 ? 64 : lo);
-        hi = hi < 0 ? 0 : (hi > 64 ? 64 : hi);
-        if (hi <= lo) return 0ull;
-        const uint64_t up = hi == 64 ? ~0ull : ((1ull << hi) - 1ull);
-        return up & ~((1ull << lo) - 1ull);
+    // sklearn's step of coordinate j from its lane's values (oracle/lasso_oracle.c):
+    // H[j] after the first axpy is lane j's own fma (r = Q[j][j] there), then
+    // fsign(tmp) * fmax(|tmp| - alpha, 0) / (qii + beta) by Markstein's correction (above) with its first
+    // product as m * (fsign(tmp) * r): the sign is exact (+-1, or 0 with m = 0), so that product
+    // is the same double and the sign multiply leaves the chain.  Lane cl decides the (uniform)
+    // IEEE-division branch: a divisor without a normal reciprocal has r = 0, so qt0 = 0 takes it.
+    auto solve = [&](double qv, double hv, double wv, double qdv, double ddv, double rdv, int cl) {
+        const double hh = wv != 0.0 ? __builtin_fma(-wv, qdv, hv) : hv;
+        const double tmp = qv - hh;
+        const double m = __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0);
+        const double sg = fsign(tmp);
+        const double num = sg * m;
+        const double qt0 = m * (sg * rdv);
+        const double et = __builtin_fma(-qt0, ddv, num);
+        double wn = __builtin_fma(et, rdv, qt0);
+        pin(wn);
+        const double aq = __builtin_fabs(qt0);
+        const uint64_t good = __builtin_amdgcn_ballot_w64(aq > 0x1p-400) &
+                              __builtin_amdgcn_ballot_w64(aq < 0x1p400);
+        if (__builtin_expect(!((good >> cl) & 1), 0)) wn = num == 0.0 ? num : num / ddv;
+        if (POS && tmp < 0) wn = 0.0;
+        return wn;
     };
     for (n_iter = 0; n_iter < max_iter; ++n_iter) {
-        double w_max = 0.0, d_w_max = 0.0;
-        for (int ii = 0; ii < p; ++ii) {
-            {   // skip coordinates [ii, next) that cannot move (exactly sklearn's no-ops)
-                const uint64_t m0 = moves(q0, h0, w0) & live0 & span(ii, 64);
-                const uint64_t m1 = moves(q1, h1, w1) & live1 & span(ii - 64, 64);
-                const int next = __builtin_amdgcn_readfirstlane(
-                    m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : p));
-                if (next > ii) {                    // (uniform) their stored signed zeros
-                    const uint64_t z0 = live0 & span(ii, next), z1 = live1 & span(ii - 64, next - 64);
-                    if (__builtin_amdgcn_inverse_ballot_w64(z0)) w0 = zero_of(q0, h0);
-                    if (__builtin_amdgcn_inverse_ballot_w64(z1)) w1 = zero_of(q1, h1);
-                    ii = next;
-                    if (ii >= p) break;
-                }
+        // Each coordinate is visited once per sweep, so its d_w is |w at the sweep's end - w at
+        // its start| and both maxima are taken once per sweep (fmax: the same values).  The
+        // signed zero a skipped coordinate stores (sklearn's fsign(tmp) * 0 / (qii + beta)) is
+        // the sign of q - h at its visit, i.e. after the last update before it: every update c
+        // records that sign for the lanes above c (ZN), and the lanes that were zero before and
+        // after their visit take it at the sweep's end.  Coordinates that cannot move are exactly
+        // sklearn's no-ops; the next movable one is found by ballot over the lanes' current H.
+        const double ws0 = w0, ws1 = w1;
+        uint64_t ZN0 = 0, ZN1 = 0;
+        int c = -1;
+        uint64_t ab0 = ~0ull, ab1 = ~0ull;   // the lanes of each half above c
+        for (;;) {
+            const double t0 = q0 - h0, t1 = q1 - h1;
+            if constexpr (!POS) {
+                ZN0 = (ZN0 & ~ab0) | (__builtin_amdgcn_ballot_w64(t0 < 0.0) & ab0);
+                ZN1 = (ZN1 & ~ab1) | (__builtin_amdgcn_ballot_w64(t1 < 0.0) & ab1);
             }
-            // (the ballot above never stops at a coordinate with a zero diagonal: not movable)
-            const double* row = Q + ii * kQS;          // (zero past column p: no lane masks)
-            const double r0 = row[j0], r1 = row[j1];
-            const double qii = cqd[ii];
-            const double w_ii = pick(w0, w1, ii);
-            // H[ii] after the first axpy is lane ii's own fma (r = Q[ii][ii] there): computed on
-            // the scalar path directly, so the step does not wait for the row read or the axpy
-            const double h_ii = pick(h0, h1, ii);
-            const double hh = w_ii != 0.0 ? __builtin_fma(-w_ii, qii, h_ii) : h_ii;
+            // movable (with its nonzero diagonal): w != 0, or the soft threshold of q - h is
+            // nonzero -- fmax(|t| - alpha, 0) != 0 is |t| > alpha (NaN: false)
+            const uint64_t m0 = (__builtin_amdgcn_ballot_w64(w0 != 0.0) |
+                                 __builtin_amdgcn_ballot_w64(POS ? t0 > alpha : __builtin_fabs(t0) > alpha)) &
+                                live0 & ab0;
+            const uint64_t m1 = (__builtin_amdgcn_ballot_w64(w1 != 0.0) |
+                                 __builtin_amdgcn_ballot_w64(POS ? t1 > alpha : __builtin_fabs(t1) > alpha)) &
+                                live1 & ab1;
+            const int f0 = __builtin_ctzg(m0, 64), f1 = __builtin_ctzg(m1, 64);
+            const int f = f0 < 64 ? f0 : 64 + f1;
+            c = __builtin_amdgcn_readfirstlane(f < p ? f : p);
+            if (c >= p) break;
+            // (the masks never name a coordinate with a zero diagonal: not movable)
+            const double* row = Q + c * kQS;          // (zero past column p: no lane masks)
+            const double r0 = row[j0], r1 = row[j1];  // (read now, used by the axpys)
+            const int cl = c & 63;
+            double wn, w_c;
+            // the coordinate's step runs on its half's registers, every lane of the half at once
+            // (lane cl's is the one kept): its weight, H, q, diagonal and reciprocal are already
+            // there -- no broadcast or table read ahead of the chain
+            if (c < 64) {
+                ab0 = ~1ull << cl;
+                w_c = bcast(w0, cl);
+                const double wv = solve(q0, h0, w0, qd0, dd0, rd0, cl);
+                wn = bcast(wv, cl);
+                w0 = lane == cl ? wv : w0;
+            } else {
+                ab0 = 0ull;
+                ab1 = ~1ull << cl;
+                w_c = bcast(w1, cl);
+                const double wv = solve(q1, h1, w1, qd1, dd1, rd1, cl);
+                wn = bcast(wv, cl);
+                w1 = lane == cl ? wv : w1;
+            }
             // the axpys run unconditionally: with a zero weight fma(+-0, r, h) = h for the finite
             // Gram (a zero h may change the sign of its zero, which reaches no weight: h enters
             // only through q - h and further fmas)
-            h0 = __builtin_fma(-w_ii, r0, h0);
-            h1 = __builtin_fma(-w_ii, r1, h1);
-            const double tmp = cq[ii] - hh;
-            double wn;
-            if (POS && tmp < 0) {
-                wn = 0.0;
-            } else {
-                // (a divisor without a normal reciprocal has rd = 0: q0 = 0 takes div_r's IEEE
-                // branch)
-                const double num = fsign(tmp) * __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0);
-                wn = div_r(num, qii + beta, crd[ii]);
-            }
-            w0 = lane == ii ? wn : w0;
-            w1 = lane + 64 == ii ? wn : w1;
-            h0 = __builtin_fma(wn, r0, h0);
-            h1 = __builtin_fma(wn, r1, h1);
-            // NaN-free: fmax keeps the larger, as the comparisons did
-            d_w_max = __builtin_fmax(__builtin_fabs(wn - w_ii), d_w_max);
-            w_max = __builtin_fmax(__builtin_fabs(wn), w_max);
+            h0 = __builtin_fma(wn, r0, __builtin_fma(-w_c, r0, h0));
+            h1 = __builtin_fma(wn, r1, __builtin_fma(-w_c, r1, h1));
         }
+        if constexpr (!POS) {
+            // zero before and after the visit (skipped): the sign of q - h there
+            if (((live0 >> lane) & 1) && ws0 == 0.0 && w0 == 0.0) w0 = ((ZN0 >> lane) & 1) ? -0.0 : 0.0;
+            if (((live1 >> lane) & 1) && ws1 == 0.0 && w1 == 0.0) w1 = ((ZN1 >> lane) & 1) ? -0.0 : 0.0;
+        }
+        const double d_w_max = wave_max(__builtin_fmax(__builtin_fabs(w0 - ws0), __builtin_fabs(w1 - ws1)));
+        const double w_max = wave_max(__builtin_fmax(__builtin_fabs(w0), __builtin_fabs(w1)));
         if (w_max == 0.0 || d_w_max / w_max < d_w_tol || n_iter == max_iter - 1) {
             double q_dot_w = 0.0, wh = 0.0, w_norm2 = 0.0, asum = 0.0, dual = 0.0;
             for (int j = 0; j < p; ++j) {

@@ -117,8 +117,9 @@ def test_lasso_rejects_nonfinite():
 @pytest.mark.parametrize("p,alpha,pos", [(96, 2e-4, 0), (110, 5e-5, 0), (70, 1e-4, 1)])
 def test_kernel_dense_fit_bit_exact_vs_oracle(p, alpha, pos):
     """Dense fits (many coefficients move every sweep, hundreds of sweeps, both column halves):
-    the kernel's pipelined coordinate step -- the next nonzero coordinate's row and H read while
-    the current one computes -- against the oracle's sequential descent, bit for bit."""
+    the kernel's pipelined coordinate step -- the next movable coordinate's inputs read while the
+    current one computes, confirmed by the ballot after its update -- against the oracle's
+    sequential descent, bit for bit (signed zeros included)."""
     import torch
     import oracle
     from afm import _lib
@@ -140,5 +141,33 @@ def test_kernel_dense_fit_bit_exact_vs_oracle(p, alpha, pos):
         wo, gap, tol_y, it = oracle.lasso_gram(Q, q, yy, alpha * nn, max_iter=10000, tol=tol,
                                                positive=bool(pos))
         assert (wo != 0).sum() >= 10 and it >= 5
-        assert np.array_equal(w.cpu().numpy(), wo)
+        assert w.cpu().numpy().tobytes() == wo.tobytes()
         assert info.cpu().numpy().tolist() == [gap, tol_y, float(it)]
+
+
+@pytest.mark.gpu
+def test_kernel_engine_dense_gram_bit_exact_vs_oracle(golden_dir):
+    """The bench's `dense_lasso` fit itself: the engine's pooled Gram of the config-C dense
+    variant (tests/golden/lasso_dense_gram.npz, saved by `LASSO_SAVE=<dir> tools/lasso_probe.py`
+    from the engine's own pooled moments: 96 features, alpha 2e-6, 1,936 sweeps, 20 nonzero
+    coefficients) -- afm_lasso_fit_f64 against the oracle's descent on the same moments, bit for
+    bit (signed zeros included), and the fit's coefficients and sweep count as saved."""
+    import torch
+    import oracle
+    from afm import _lib
+    d = np.load(os.path.join(golden_dir, "lasso_dense_gram.npz"))
+    p, alpha, max_iter, tol = int(d["p"]), float(d["alpha"]), int(d["max_iter"]), float(d["tol"])
+    G = torch.from_numpy(d["gram"]).cuda().contiguous()
+    S = torch.from_numpy(d["shift"]).cuda().contiguous()
+    beta = torch.empty(p + 1, dtype=torch.float64, device="cuda")
+    info = torch.empty(3, dtype=torch.float64, device="cuda")
+    h = _lib.Context.get(0).bind_stream()
+    _lib.check(_lib.lib().afm_lasso_fit_f64(h, _lib.ptr(G), _lib.ptr(S), p, alpha, max_iter, tol,
+                                            0, _lib.ptr(beta), _lib.ptr(info)))
+    nn, Q, q, yy = oracle.centered_moments(d["gram"][0])
+    wo, gap, tol_y, it = oracle.lasso_gram(Q, q, yy, alpha * nn, max_iter=max_iter, tol=tol)
+    b = beta.cpu().numpy()
+    assert it == 1936 and (wo != 0).sum() == 20
+    assert b[1:].tobytes() == wo.tobytes()
+    assert info.cpu().numpy().tolist() == [gap, tol_y, float(it)]
+    assert b.tobytes() == d["beta"].tobytes()

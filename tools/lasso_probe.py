@@ -41,6 +41,12 @@ def main():
                        "lasso")
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
+        if os.environ.get("LASSO_SAVE"):
+            import numpy as np
+            np.savez(os.path.join(os.environ["LASSO_SAVE"], f"lasso_{name}_gram.npz"),
+                     gram=pipe.pool_g.cpu().numpy(), shift=pipe.pool_s.cpu().numpy(),
+                     p=pipe.p, alpha=cfg.alpha, max_iter=cfg.max_iter, tol=cfg.lasso_tol,
+                     beta=beta.cpu().numpy(), info=info.cpu().numpy())
         it = int(info[2].item())
         ms = sorted(ts)[len(ts) // 2]
         dig = hashlib.sha1(beta.cpu().numpy().tobytes()).hexdigest()[:12]
