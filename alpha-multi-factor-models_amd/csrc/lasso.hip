@@ -125,64 +125,50 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
         if (POS && tmp < 0) wn = 0.0;
         return wn;
     };
-    for (n_iter = 0; n_iter < max_iter; ++n_iter) {
-        // Each coordinate is visited once per sweep, so its d_w is |w at the sweep's end - w at
-        // its start| and both maxima are taken once per sweep (fmax: the same values).  The
-        // signed zero a skipped coordinate stores (sklearn's fsign(tmp) * 0 / (qii + beta)) is
-        // the sign of q - h at its visit, i.e. after the last update before it: every update c
-        // records that sign for the lanes above c (ZN), and the lanes that were zero before and
-        // after their visit take it at the sweep's end.  Coordinates that cannot move are exactly
-        // sklearn's no-ops; the next movable one is found by ballot over the lanes' current H.
-        const double ws0 = w0, ws1 = w1;
-        uint64_t ZN0 = 0, ZN1 = 0;
-        int c = -1;
-        uint64_t ab0 = ~0ull, ab1 = ~0ull;   // the lanes of each half above c
+    // One half's part of a sweep: coordinates are visited in increasing order, so a sweep runs
+    // all moves of features 0..63, then all of 64..; within a half the step runs on that half's
+    // registers in every lane at once (lane c's result kept): its weight, H, q, diagonal and
+    // reciprocal are already there.  Each scan over the half's lanes above the last move records
+    // the sign of q - h (ZN: what a lane skipped there stores) and finds the next movable one
+    // (with its nonzero diagonal: w != 0, or the soft threshold of q - h is nonzero --
+    // fmax(|t| - alpha, 0) != 0 is |t| > alpha, NaN: false).  Coordinates that cannot move are
+    // exactly sklearn's no-ops.
+    auto half = [&](double& qh, double& hh, double& wh, double qdh, double ddh, double rdh,
+                    uint64_t liveh, uint64_t& ZN, int base) {
+        uint64_t ab = ~0ull;                 // the half's lanes above the last move
         for (;;) {
-            const double t0 = q0 - h0, t1 = q1 - h1;
-            if constexpr (!POS) {
-                ZN0 = (ZN0 & ~ab0) | (__builtin_amdgcn_ballot_w64(t0 < 0.0) & ab0);
-                ZN1 = (ZN1 & ~ab1) | (__builtin_amdgcn_ballot_w64(t1 < 0.0) & ab1);
-            }
-            // movable (with its nonzero diagonal): w != 0, or the soft threshold of q - h is
-            // nonzero -- fmax(|t| - alpha, 0) != 0 is |t| > alpha (NaN: false)
-            const uint64_t m0 = (__builtin_amdgcn_ballot_w64(w0 != 0.0) |
-                                 __builtin_amdgcn_ballot_w64(POS ? t0 > alpha : __builtin_fabs(t0) > alpha)) &
-                                live0 & ab0;
-            const uint64_t m1 = (__builtin_amdgcn_ballot_w64(w1 != 0.0) |
-                                 __builtin_amdgcn_ballot_w64(POS ? t1 > alpha : __builtin_fabs(t1) > alpha)) &
-                                live1 & ab1;
-            const int f0 = __builtin_ctzg(m0, 64), f1 = __builtin_ctzg(m1, 64);
-            const int f = f0 < 64 ? f0 : 64 + f1;
-            c = __builtin_amdgcn_readfirstlane(f < p ? f : p);
-            if (c >= p) break;
+            const double t = qh - hh;
+            if constexpr (!POS) ZN ^= (ZN ^ __builtin_amdgcn_ballot_w64(t < 0.0)) & ab;
+            const uint64_t mv = (__builtin_amdgcn_ballot_w64(wh != 0.0) |
+                                 __builtin_amdgcn_ballot_w64(POS ? t > alpha : __builtin_fabs(t) > alpha)) &
+                                liveh & ab;
+            if (mv == 0) break;
+            const int cl = __builtin_amdgcn_readfirstlane(__builtin_ctzll(mv));
             // (the masks never name a coordinate with a zero diagonal: not movable)
-            const double* row = Q + c * kQS;          // (zero past column p: no lane masks)
-            const double r0 = row[j0], r1 = row[j1];  // (read now, used by the axpys)
-            const int cl = c & 63;
-            double wn, w_c;
-            // the coordinate's step runs on its half's registers, every lane of the half at once
-            // (lane cl's is the one kept): its weight, H, q, diagonal and reciprocal are already
-            // there -- no broadcast or table read ahead of the chain
-            if (c < 64) {
-                ab0 = ~1ull << cl;
-                w_c = bcast(w0, cl);
-                const double wv = solve(q0, h0, w0, qd0, dd0, rd0, cl);
-                wn = bcast(wv, cl);
-                w0 = lane == cl ? wv : w0;
-            } else {
-                ab0 = 0ull;
-                ab1 = ~1ull << cl;
-                w_c = bcast(w1, cl);
-                const double wv = solve(q1, h1, w1, qd1, dd1, rd1, cl);
-                wn = bcast(wv, cl);
-                w1 = lane == cl ? wv : w1;
-            }
+            const double* row = Q + (base + cl) * kQS;   // (zero past column p: no lane masks)
+            const double r0 = row[j0], r1 = row[j1];
+            const double w_c = bcast(wh, cl);
+            const double wv = solve(qh, hh, wh, qdh, ddh, rdh, cl);
+            const double wn = bcast(wv, cl);
+            wh = lane == cl ? wv : wh;
             // the axpys run unconditionally: with a zero weight fma(+-0, r, h) = h for the finite
             // Gram (a zero h may change the sign of its zero, which reaches no weight: h enters
             // only through q - h and further fmas)
             h0 = __builtin_fma(wn, r0, __builtin_fma(-w_c, r0, h0));
             h1 = __builtin_fma(wn, r1, __builtin_fma(-w_c, r1, h1));
+            ab = ~1ull << cl;
         }
+    };
+    for (n_iter = 0; n_iter < max_iter; ++n_iter) {
+        // Each coordinate is visited once per sweep, so its d_w is |w at the sweep's end - w at
+        // its start| and both maxima are taken once per sweep (fmax: the same values).  The
+        // signed zero a skipped coordinate stores (sklearn's fsign(tmp) * 0 / (qii + beta)) is
+        // the sign of q - h at its visit, i.e. after the last update before it (ZN), applied to
+        // the lanes that were zero before and after their visit at the sweep's end.
+        const double ws0 = w0, ws1 = w1;
+        uint64_t ZN0 = 0, ZN1 = 0;
+        half(q0, h0, w0, qd0, dd0, rd0, live0, ZN0, 0);
+        half(q1, h1, w1, qd1, dd1, rd1, live1, ZN1, 64);
         if constexpr (!POS) {
             // zero before and after the visit (skipped): the sign of q - h there
             if (((live0 >> lane) & 1) && ws0 == 0.0 && w0 == 0.0) w0 = ((ZN0 >> lane) & 1) ? -0.0 : 0.0;
