@@ -109,7 +109,9 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     // is the same double and the sign multiply leaves the chain.  Lane cl decides the (uniform)
     // IEEE-division branch: a divisor without a normal reciprocal has r = 0, so qt0 = 0 takes it.
     auto solve = [&](double qv, double hv, double wv, double qdv, double ddv, double rdv, int cl) {
-        const double hh = wv != 0.0 ? __builtin_fma(-wv, qdv, hv) : hv;
+        // (with a zero weight: fma(-+0, qii, h) differs from h at most in the sign of a zero h,
+        // which changes tmp only between +0 and -0 -- the same weight either way)
+        const double hh = __builtin_fma(-wv, qdv, hv);
         const double tmp = qv - hh;
         const double m = __builtin_fmax(__builtin_fabs(tmp) - alpha, 0.0);
         const double sg = fsign(tmp);
@@ -136,13 +138,14 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     auto half = [&](double& qh, double& hh, double& wh, double qdh, double ddh, double rdh,
                     uint64_t liveh, uint64_t& ZN, int base) {
         uint64_t ab = ~0ull;                 // the half's lanes above the last move
-        for (;;) {
+        auto scan = [&]() -> uint64_t {
             const double t = qh - hh;
             if constexpr (!POS) ZN ^= (ZN ^ __builtin_amdgcn_ballot_w64(t < 0.0)) & ab;
-            const uint64_t mv = (__builtin_amdgcn_ballot_w64(wh != 0.0) |
-                                 __builtin_amdgcn_ballot_w64(POS ? t > alpha : __builtin_fabs(t) > alpha)) &
-                                liveh & ab;
-            if (mv == 0) break;
+            return (__builtin_amdgcn_ballot_w64(wh != 0.0) |
+                    __builtin_amdgcn_ballot_w64(POS ? t > alpha : __builtin_fabs(t) > alpha)) &
+                   liveh & ab;
+        };
+        for (uint64_t mv = scan(); mv; mv = scan()) {
             const int cl = __builtin_amdgcn_readfirstlane(__builtin_ctzll(mv));
             // (the masks never name a coordinate with a zero diagonal: not movable)
             const double* row = Q + (base + cl) * kQS;   // (zero past column p: no lane masks)
