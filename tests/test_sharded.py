@@ -133,10 +133,14 @@ def _paths_worker(rank, world, port, outdir):
     lo, hi = even_range(npaths, world, rank)
     loc = {k: torch.arange(lo, hi, dtype=torch.float64)[:, None] * 10 + torch.arange(steps + (k == "value"))
            for k in ("value", "turnover", "long_ret", "short_ret")}
-    out = gather_path_series(loc, npaths, Comm())
+    cm = Comm()
+    out = gather_path_series(loc, npaths, cm)
     want = torch.arange(npaths, dtype=torch.float64)[:, None] * 10
     assert torch.equal(out["value"], want + torch.arange(steps + 1))
     assert torch.equal(out["turnover"], want + torch.arange(steps))
+    # (no rank leaves while a peer may still be reading the last collective from its socket:
+    # gloo aborts a peer whose connection closes mid-transfer)
+    cm.barrier()
     (Path(outdir) / f"paths{rank}").write_text("ok")
 
 
