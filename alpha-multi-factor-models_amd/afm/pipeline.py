@@ -779,17 +779,22 @@ class Pipeline:
     def _place(self, dst, gathered, rows=None):
         """Scatter per-rank shard columns ([W][rows][wide]) into a full-width plane.  Rank q's
         columns start at q * wide (the fixed block split), so the ranks side by side ARE the
-        plane's first W * wide columns: one reorder copy and one copy, not one per rank (each
-        small copy is a launch the step waits on)."""
+        plane's first W * wide columns: the full-width ranks in ONE strided copy straight into the
+        plane (no reordered intermediate), the last (short) rank in a second -- not one copy per
+        rank (each small copy is a launch the step waits on).  Columns from A on are untouched."""
         A = self.ranges[-1][1]
         if A == 0:
             return
         W, nr, wide = gathered.shape[0], gathered.shape[1], gathered.shape[2]
+        d = dst if rows is None else dst[rows]
+        k = (W - 1) * wide                  # the full-width ranks' columns
+        if k <= A and A - k <= wide:
+            if W > 1:
+                d[:, :k].view(nr, W - 1, wide).copy_(gathered[:W - 1].permute(1, 0, 2))
+            d[:, k:A] = gathered[W - 1, :, :A - k]
+            return
         side = gathered.permute(1, 0, 2).reshape(nr, W * wide)
-        if rows is None:
-            dst[:, :A] = side[:, :A]
-        else:
-            dst[rows, :A] = side[:, :A]
+        d[:, :A] = side[:, :A]
 
     def _gather_test_planes(self):
         import torch

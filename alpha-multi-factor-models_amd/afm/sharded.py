@@ -73,7 +73,13 @@ class Comm:
         g = self.all_gather(torch.cat(flat))                     # [world, total bytes]
         out, off = [], 0
         for t, n in zip(tensors, sizes):
-            part = g[:, off:off + n].contiguous().view(t.dtype)
+            # a strided view of the gathered bytes when the part's offset and the row stride are
+            # multiples of its element size (no copy of the gathered buffer), else a copy
+            es = t.element_size()
+            part = g[:, off:off + n]
+            if off % es or g.shape[1] % es:
+                part = part.contiguous()
+            part = part.view(t.dtype)
             out.append(part.view((self.world,) + tuple(t.shape)))
             off += n
         return out
