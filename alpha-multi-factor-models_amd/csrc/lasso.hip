@@ -106,8 +106,13 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
     // H[j] after the first axpy is lane j's own fma (r = Q[j][j] there), then
     // fsign(tmp) * fmax(|tmp| - alpha, 0) / (qii + beta) by Markstein's correction (above) with its first
     // product as m * (fsign(tmp) * r): the sign is exact (+-1, or 0 with m = 0), so that product
-    // is the same double and the sign multiply leaves the chain.  Lane cl decides the (uniform)
-    // IEEE-division branch: a divisor without a normal reciprocal has r = 0, so qt0 = 0 takes it.
+    // is the same double and the sign multiply leaves the chain.  Returns lane cl's weight,
+    // broadcast.  The IEEE-division branch is decided on that broadcast (scalar exponent test, no
+    // vector compare on the chain): a quotient whose exponent is inside [2^-398, 2^399) has its
+    // first product inside (2^-400, 2^400), where the Markstein step is the IEEE quotient; any
+    // other (zero -- a zero numerator, or r = 0 for a divisor without a normal reciprocal --
+    // subnormal, huge, inf, NaN) takes the division.  Both give the correctly rounded quotient
+    // wherever both apply, so the narrower test changes no bit.
     auto solve = [&](double qv, double hv, double wv, double qdv, double ddv, double rdv, int cl) {
         // (with a zero weight: fma(-+0, qii, h) differs from h at most in the sign of a zero h,
         // which changes tmp only between +0 and -0 -- the same weight either way)
@@ -118,13 +123,13 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
         const double num = sg * m;
         const double qt0 = m * (sg * rdv);
         const double et = __builtin_fma(-qt0, ddv, num);
-        double wn = __builtin_fma(et, rdv, qt0);
-        pin(wn);
-        const double aq = __builtin_fabs(qt0);
-        const uint64_t good = __builtin_amdgcn_ballot_w64(aq > 0x1p-400) &
-                              __builtin_amdgcn_ballot_w64(aq < 0x1p400);
-        if (__builtin_expect(!((good >> cl) & 1), 0)) wn = num == 0.0 ? num : num / ddv;
-        if (POS && tmp < 0) wn = 0.0;
+        double wn = bcast(__builtin_fma(et, rdv, qt0), cl);
+        const uint32_t ex = (uint32_t)(__builtin_bit_cast(uint64_t, wn) >> 52) & 0x7ffu;
+        if (__builtin_expect(ex - (1023u - 398u) >= 797u, 0))
+            wn = bcast(num == 0.0 ? num : num / ddv, cl);
+        if constexpr (POS) {
+            if ((__builtin_amdgcn_ballot_w64(tmp < 0) >> cl) & 1) wn = 0.0;
+        }
         return wn;
     };
     // One half's part of a sweep: coordinates are visited in increasing order, so a sweep runs
@@ -151,9 +156,8 @@ __global__ __launch_bounds__(kLassoThreads) void lasso_cd_kernel(const double* g
             const double* row = Q + (base + cl) * kQS;   // (zero past column p: no lane masks)
             const double r0 = row[j0], r1 = row[j1];
             const double w_c = bcast(wh, cl);
-            const double wv = solve(qh, hh, wh, qdh, ddh, rdh, cl);
-            const double wn = bcast(wv, cl);
-            wh = lane == cl ? wv : wh;
+            const double wn = solve(qh, hh, wh, qdh, ddh, rdh, cl);
+            wh = lane == cl ? wn : wh;
             // the axpys run unconditionally: with a zero weight fma(+-0, r, h) = h for the finite
             // Gram (a zero h may change the sign of its zero, which reaches no weight: h enters
             // only through q - h and further fmas)
