@@ -412,6 +412,13 @@ class Pipeline:
             if not self.stream_z:
                 self.zstats_done = torch.cuda.Event()
 
+    @property
+    def labels_in_factor_stage(self) -> bool:
+        """The two label planes are written inside the ``factors`` stage (main stream) rather
+        than on a side stream beside it: one GPU with ``labels_side`` off (bench.py's roofline
+        counts their bytes against that stage only then)."""
+        return self.W == 1 and not self.cfg.labels_side
+
     def n_asset_days_local(self) -> int:
         return int(self.g.valid.sum().item())
 
@@ -473,21 +480,23 @@ class Pipeline:
                                     P(self.fm_beta_own), P(self.fm_nobs_own),
                                     P(self.fm_rank_own)), "fm solve")
 
-    def _factors_streamed(self, h, mark):
+    def _factors_streamed(self, h, lab_side, mark):
         """The factor panel in time slabs (zbounds) on the main stream, each slab's all_df rows
         right behind it, and the train window's z statistics streamed slab by slab on the side
         stream as each slab lands (afm_zscore_stats_slab_f64, every (feature, asset) recurrence
         carried): bitwise the panel, statistics and row sets of one call each.  The label planes
         go first, once, on the second side stream (inputs only; tmr_ret1d is a feature) -- not
-        inside every factor slab."""
+        inside every factor slab; with ``labels_side`` off, on the main stream ahead of the first
+        slab, inside the factors stage)."""
         import torch
         L, P, chk = _lib.lib(), _lib.ptr, _lib.check
         g, sp, T, lda_r, p, A_r = self.g, self.sp, self.T, self.lda_r, self.p, self.A_r
-        with torch.cuda.stream(self.side2):
+        lab_stream = self.side2 if lab_side else self.main
+        with torch.cuda.stream(lab_stream):
             h2 = self.ctx.bind_stream()
             chk(L.afm_labels_f64(h2, T, lda_r, 0, T, P(g.excess), P(g.ret1d), P(g.vbits),
                                  P(self.out[TARGET]), P(self.out[TMR])), "labels")
-            self.labels_done.record(self.side2)
+            self.labels_done.record(lab_stream)
         h = self.ctx.bind_stream()
         b, tr1 = self.zbounds, sp.tr1
         for i in range(len(b) - 1):
@@ -604,7 +613,7 @@ class Pipeline:
             # (it runs on the CUs the factor workgroups leave free); zstats waits for them
             lab_side = W == 1 and c.labels_side
             if self.stream_z:
-                self._factors_streamed(h, mark)
+                self._factors_streamed(h, lab_side, mark)
                 h = self.ctx.bind_stream()
             elif self.early:
                 self._factors_early(h, lab_side, mark)

@@ -21,16 +21,7 @@ hipError_t afm_lds_opt_in(const afm_ctx* ctx, const void* kernel, int bytes) {
     return e;
 }
 
-int afm_ctx_cus(afm_ctx* ctx) {
-    if (ctx->ncu <= 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, ctx->device) !=
-                hipSuccess || n <= 0)
-            n = 256;                                            // MI355X
-        ctx->ncu = n;
-    }
-    return ctx->ncu;
-}
+int afm_ctx_cus(afm_ctx* ctx) { return ctx->ncu; }
 
 extern "C" {
 
@@ -43,9 +34,15 @@ int afm_ctx_create(int device, afm_ctx** out) {
     int n = 0;
     AFM_HIP(hipGetDeviceCount(&n));
     AFM_CHECK_ARG(device >= 0 && device < n, "device ordinal out of range");
-    AFM_HIP(hipSetDevice(device));
+    // the CU count is read once here (no lazy init shared between host threads), and the
+    // caller's current device is left as it was
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        ncu <= 0)
+        ncu = 256;                                              // MI355X
     afm_ctx* c = new afm_ctx();
     c->device = device;
+    c->ncu = ncu;
     *out = c;
     return AFM_OK;
 }

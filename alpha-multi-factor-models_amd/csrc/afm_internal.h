@@ -43,12 +43,12 @@ struct afm_ctx {
     // the lock guarding it (host threads may share a context)
     std::unordered_map<const void*, int> slab_types;
     std::mutex slab_mu;
-    // compute units of the device (hipDeviceAttributeMultiprocessorCount), read once: launch
-    // shapes that fill the chip are chosen from it (0 = not read yet)
-    int ncu = 0;
+    // compute units of the device (hipDeviceAttributeMultiprocessorCount), read once by
+    // afm_ctx_create: launch shapes that fill the chip are chosen from it
+    int ncu = 256;
 };
 
-// the context device's compute-unit count (cached in the context)
+// the context device's compute-unit count (read when the context was created)
 int afm_ctx_cus(afm_ctx* ctx);
 
 void afm_set_error(const std::string& msg);
@@ -75,11 +75,32 @@ hipError_t afm_lds_opt_in(const afm_ctx* ctx, const void* kernel, int bytes);
         }                                                                                 \
     } while (0)
 
-#define AFM_CTX(ctx)                                                      \
-    do {                                                                  \
-        if (!(ctx) || (ctx)->magic != 0x61666d31) {                       \
-            afm_set_error(std::string(__func__) + ": invalid afm_ctx");  \
-            return AFM_E_STATE;                                           \
-        }                                                                 \
-        AFM_HIP(hipSetDevice((ctx)->device));                             \
-    } while (0)
+// Every entry point runs on its context's device and hands the calling thread's current device
+// back on every exit path (torch and other callers rely on it): AFM_CTX validates the context and
+// declares this guard in the entry point's scope.
+struct afm_device_guard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit afm_device_guard(int device) {
+        err = hipGetDevice(&prev);
+        if (err == hipSuccess && prev != device) err = hipSetDevice(device);
+        else prev = -1;                                 // already current: nothing to restore
+    }
+    ~afm_device_guard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    afm_device_guard(const afm_device_guard&) = delete;
+    afm_device_guard& operator=(const afm_device_guard&) = delete;
+};
+
+#define AFM_CTX(ctx)                                                                      \
+    if (!(ctx) || (ctx)->magic != 0x61666d31) {                                           \
+        afm_set_error(std::string(__func__) + ": invalid afm_ctx");                      \
+        return AFM_E_STATE;                                                               \
+    }                                                                                     \
+    const afm_device_guard afm_dev_guard_((ctx)->device);                                 \
+    if (afm_dev_guard_.err != hipSuccess) {                                               \
+        afm_set_error(std::string(__func__) + ": hipSetDevice: " +                        \
+                      hipGetErrorString(afm_dev_guard_.err));                             \
+        return AFM_E_HIP;                                                                 \
+    }

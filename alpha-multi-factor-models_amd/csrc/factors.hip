@@ -2307,8 +2307,8 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
             }
         }
     }
-    if (full) {
-        nanfree_bits += (t0 / 64) * lda;
+    if (full) {                       // (null on the ext_part path: the masks come later)
+        if (nanfree_bits) nanfree_bits += (t0 / 64) * lda;
         if (finite_bits) finite_bits += (t0 / 64) * lda;
     }
     const int64_t nblk = (A + 63) / 64;
@@ -2511,10 +2511,9 @@ extern "C" int afm_factors_range_part_f64(afm_ctx* ctx, int64_t T, int64_t A, in
     AFM_CHECK_ARG(T <= (int64_t)1 << 31, "T too large");
     AFM_CHECK_ARG(0 <= t0 && t0 < t1 && t1 <= T && t0 % 64 == 0 && (t1 % 64 == 0 || t1 == T),
                   "need 0 <= t0 < t1 <= T with t0 and t1 (unless T) multiples of 64");
-    // (the bit-word pointers are not written on this path: the masks come later)
-    uint64_t dummy = 0;
+    // (no bit-word pointers on this path: the masks come later, afm_factor_masks_f64)
     return factors_slab(ctx, T, A, lda, t0, t1, close, volume, nullptr, nullptr, valid_bits, out,
-                        &dummy, nullptr, state, true, part);
+                        nullptr, nullptr, state, true, part);
 }
 
 extern "C" int afm_factor_masks_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t t0,

@@ -1829,33 +1829,28 @@ __global__ __launch_bounds__(256) void turnover_terms_wave_kernel(int64_t nd, co
         const bool node = lane < ni;
         const int pnext = wv_pull(pos_o, lane < 63 ? lane + 1 : 63);
         const int dep = node ? np_lca_depth(n, pos_o, pnext) : 0x3fffffff;
-        // nearest strictly shallower node on each side (-1: none).  The depths of one summation
-        // tree span < 4 kMaxLevels values; a wider span means union positions that do not belong
-        // to this step's union (inconsistent inputs): an error record, not a long loop
+        // nearest strictly shallower node on each side (-1: none), visiting the depths in
+        // increasing order.  A dense span (the usual case: the depths of one summation tree over a
+        // few thousand slots) steps d by one with one ballot each; a wide span (a union of ~1.8 M
+        // slots or more) visits only the depths present, the next one by a wave minimum -- at
+        // most ni <= 63 of them -- so the record is the LDS kernel's for any union size
         int nl = -1, nr = -1;
         const int dlo = wv_min(dep), dhi = wv_max(node ? dep : -1);
-        if (dhi - dlo >= 4 * kMaxLevels) {
-            if (lane == 0) {
-                R[0] = -2;
-                R[1] = 0;
-                R[2] = 0;
-                R[3] = 0;
-                rlen[i] = 4;
-            }
-            continue;
-        }
+        const bool dense = dhi - dlo < 4 * kMaxLevels;
         {
             uint64_t sh = 0;                                       // nodes shallower than d
-            for (int d = dlo; d <= dhi; ++d) {
+            for (int d = dlo; d <= dhi;) {
                 const bool at = node && dep == d;
                 const uint64_t e = __ballot(at);
-                if (e == 0) continue;
-                if (at) {
-                    const uint64_t lm = sh & below, rm = sh & above;
-                    nl = lm ? 63 - __builtin_clzll(lm) : -1;
-                    nr = rm ? __builtin_ctzll(rm) : -1;
+                if (e != 0) {
+                    if (at) {
+                        const uint64_t lm = sh & below, rm = sh & above;
+                        nl = lm ? 63 - __builtin_clzll(lm) : -1;
+                        nr = rm ? __builtin_ctzll(rm) : -1;
+                    }
+                    sh |= e;
                 }
-                sh |= e;
+                d = dense ? d + 1 : wv_min(node && dep > d ? dep : 0x7fffffff);
             }
         }
         // parent = the deeper of the two; a node is its parent's left child when the parent is on

@@ -13,14 +13,19 @@ KKT weights for top/bottom-10 books on every test date + PnL/turnover scan (KKT:
 streams: AlphaSignalAnalyzer on the predictions (KKT:630-631) and the per-date FM30 OLS +
 Fama-MacBeth (north-star extension).
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 is launched by torch.distributed.run
-(one rank per GPU).  Rank 0 prints ONE JSON line.
+Usage: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one rank per GPU: under
+torch.distributed.run (WORLD_SIZE set; --gpus must equal it), or, started bare, bench.py starts
+``python -m torch.distributed.run --nproc-per-node N ... bench.py`` itself as a CHILD process
+before anything imports torch or touches the GPU, passes rank 0's line through and exits with
+the child's code (self_launch below).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -137,7 +142,7 @@ def cpu_port(seed: int, assets: int = 150, days: int = 2520):
 def rooflines(pipe, stage_ms: dict, n_ad_local: int, world: int, assets: int, days: int):
     """The factor kernel (HBM) and pooled Gram (fp64 MFMA) roofline objects of one timed
     Pipeline, ranked by their stage's device time (dominant first)."""
-    labels_in = world == 1 and not pipe.cfg.labels_side
+    labels_in = world == 1 and pipe.labels_in_factor_stage
     fac_bytes = FACTOR_BYTES_PER_AD if labels_in else FACTOR_BYTES_NO_LABELS
     fac_gbs = fac_bytes * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
     p2 = pipe.p2
@@ -332,15 +337,67 @@ def variant_line(grid, cfg, steps: int, warmup: int, what: str, roof=None) -> di
     return out
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(gpus: int, argv: list) -> int:
+    """``bench.py --gpus N`` (N > 1) started without a launcher: run the same command line under
+    ``torch.distributed.run`` (one rank per GPU, rendezvous on 127.0.0.1) as a child process --
+    never exec: this process has not imported torch nor touched the GPU, and it stays the parent.
+    Rank 0's JSON line is passed through on stdout; everything else the job prints goes to
+    stderr.  Returns the child's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    log(f"[bench] --gpus {gpus}: launching {gpus} ranks: {' '.join(cmd)}")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    assert proc.stdout is not None
+    for line in proc.stdout:
+        s = line.strip()
+        if s.startswith("{") and s.endswith("}"):
+            print(s, flush=True)
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    return proc.wait()
+
+
+def launch_world(gpus) -> tuple:
+    """(world, must_self_launch) from --gpus and the launcher's WORLD_SIZE.  Under a launcher,
+    --gpus (when given) must equal WORLD_SIZE."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is not None:
+        world = int(env)
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE="
+                             f"{world} ranks")
+        return world, False
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}")
+    return n, n > 1
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default 1, or WORLD_SIZE under a launcher); N > 1 "
+                         "without a launcher starts torch.distributed.run as a child process")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--assets", type=int, default=10000)
     ap.add_argument("--days", type=int, default=5040)
     ap.add_argument("--seed", type=int, default=2023)
     ap.add_argument("--top-n", type=int, default=10)
+    ap.add_argument("--train-end", default=None, help="PipelineConfig.train_end (small panels)")
+    ap.add_argument("--valid-end", default=None, help="PipelineConfig.valid_end (small panels)")
+    ap.add_argument("--window", type=int, default=None,
+                    help="PipelineConfig.window (rolling covariance days)")
     ap.add_argument("--fm-free-cus", type=int, default=None,
                     help="PipelineConfig.fm_free_cus (CUs the FM side stream leaves free)")
     ap.add_argument("--fm-fork", default=None,
@@ -361,6 +418,11 @@ def main():
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the top_n_100 / dense_lasso secondary lines (N = 1 only)")
     args = ap.parse_args()
+    world, spawn = launch_world(args.gpus)
+    if spawn and not args.config_only:
+        if args.emulate_world:
+            raise SystemExit("bench.py: --emulate-world is a one-GPU proxy; drop --gpus")
+        sys.exit(self_launch(world, sys.argv[1:]))
 
     import numpy as np
     import torch
@@ -377,7 +439,6 @@ def main():
         print(json.dumps({"config_" + args.config_only: fn()}), flush=True)
         return
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("AFM_BENCH_BACKEND", "nccl")
@@ -405,6 +466,9 @@ def main():
         place["zstats_slabs"] = args.zstats_slabs
     if args.fm_grid is not None:
         place["fm_grid"] = args.fm_grid
+    for k in ("train_end", "valid_end", "window"):
+        if getattr(args, k) is not None:
+            place[k] = getattr(args, k)
     cfg = PipelineConfig(top_n=args.top_n, **place)
     if world > 1:
         from afm.sharded import EXCHANGE_STAGES, Comm, ShardedPipeline
@@ -451,7 +515,8 @@ def main():
 
     total_ad = n_ad
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device="cpu" if backend == "gloo" else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
 
@@ -464,6 +529,7 @@ def main():
                                   "copies (afm.sharded.EmulatedComm); no communication time"}),
               flush=True)
         return
+    final_value = pipe.summary()["final_value"] if rank == 0 else None
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         # roofline of the two dominant kernels, ranked by per-step device time: the factor panel
@@ -493,6 +559,8 @@ def main():
             "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
             "roofline": ranked[0],
             "roofline_next": ranked[1],
+            # the portfolio's last value after the timed steps (KKT:892): the same for every N
+            "final_value": final_value,
         }
         if world == 1 and not args.no_variants:
             # secondary lines the headline step never exercises: the active-set KKT QP on

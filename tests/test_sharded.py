@@ -209,8 +209,10 @@ def test_sharded_ranks_bit_identical_to_single(tmp_path, world, A, T):
     300 assets = 5 groups of 64: blocks of 64, ranks uneven (at N = 4 two ranks hold one group, one
     holds a short one, one none).  World 8 -- the geometry of the 8-GPU claim:
     1,000 assets = 16 groups, blocks of 128, so every rank owns exactly one block of the fixed
-    8-block split (rank 7 a short one of 104 assets), runs the 15-way split factor launch on its
-    shard, owns 1/8 of the FM dates (the 8-owner all_to_all) and of the rebalance dates."""
+    8-block split (rank 7 a short one of 104 assets), runs the small-grid factor launch on its
+    2-block shard (the 30-set partition PartS, code 110) with the z statistics streamed slab by
+    slab behind it, owns 1/8 of the FM dates (the 8-owner all_to_all) and of the rebalance
+    dates.  (The 15-set PartC splits are covered by test_factors_gpu.py.)"""
     import torch
     import torch.multiprocessing as mp
     import afm
