@@ -170,6 +170,14 @@ def _even(n: int, world: int, rank: int):
     return n * rank // world, n * (rank + 1) // world
 
 
+def _share_rows(ranges, stride: int, device):
+    """Rows of the per-rank shares in an all-gathered [world][stride] buffer, in global order
+    (rank q's i-th item at row q * stride + i): ONE index_select places every rank's share."""
+    import torch
+    return torch.as_tensor(np.concatenate([q * stride + np.arange(b - a) for q, (a, b)
+                                           in enumerate(ranges)]).astype(np.int64), device=device)
+
+
 class Pipeline:
     """The chain on one device, or on one rank of ``comm.world`` (``comm``: afm.sharded.Comm).
 
@@ -326,7 +334,7 @@ class Pipeline:
         self.rdates = torch.from_numpy(rd).to(dev)
         self.reb_ext = self.reb if W == 1 else reb_buffers(self.e1 - self.e0)
         self.nr_max = max(b - a for a, b in self.rrange)
-        self._reb_rows = None
+        self._reb_rows = self._fm_rows = self._an_rows = None
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         # analyzer on the test sub-grid (64-date aligned, so the bit words line up)
@@ -384,6 +392,9 @@ class Pipeline:
         else:
             self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
+        # N > 1: the sequential PnL scan on its own stream, beside the FM exchange / solve and the
+        # analyzer's gather + series that follow the rebalance (they no longer wait for it)
+        self.side3 = torch.cuda.Stream(device=dev, priority=-8 if c.main_priority else 0)
         self.labels_done = torch.cuda.Event()
         self.fwd_early = False
         # early z statistics: the first slab ends at the first 64-date boundary past the train
@@ -599,7 +610,7 @@ class Pipeline:
         T, lda_r, p, W, nch = self.T, self.lda_r, self.p, self.W, self.nch
         full = self.full
         caller = torch.cuda.current_stream(full.device)
-        for s in (self.main, self.side, self.side2):
+        for s in (self.main, self.side, self.side2, self.side3):
             s.wait_stream(caller)
 
         def mark(stage, which):
@@ -750,19 +761,32 @@ class Pipeline:
             mark("rebalance", 1)
             if fm_at == "rebalance":
                 h = fork_fm()
-            mark("pnl", 0)
             r, q = self.reb, self.pnl
-            chk(L.afm_pnl_scan_f64(h, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]),
-                                   P(r["upos"]), P(r["usize"]), c.v0, c.rate, P(q["value"]),
-                                   P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])), "pnl")
-            mark("pnl", 1)
-            if W > 1:          # FM: per-date subtrees -> date owners (issued after the main chain)
+
+            def pnl_scan(hh):
+                mark("pnl", 0)
+                chk(L.afm_pnl_scan_f64(hh, self.nd, P(r["k"]), P(r["books"]), P(r["sums"]),
+                                       P(r["upos"]), P(r["usize"]), c.v0, c.rate, P(q["value"]),
+                                       P(q["turnover"]), P(q["long_ret"]), P(q["short_ret"])),
+                    "pnl")
+                mark("pnl", 1)
+            if W == 1:
+                pnl_scan(h)
+            else:
+                # the scan on its own stream; the FM exchange (per-date subtrees -> date owners,
+                # solves, betas) and the analyzer's gather + series run beside it on the main and
+                # second side streams, issued in this order on every rank (RCCL runs a group's
+                # collectives in issue order)
+                self.side3.wait_stream(self.main)
+                with torch.cuda.stream(self.side3):
+                    pnl_scan(self.ctx.bind_stream())
+                h = self.ctx.bind_stream()
                 self.main.wait_stream(self.side)
                 self._fm_exchange()
-                if c.analyzer:  # the analyzer's per-date results, then its series (last: RCCL
-                    with torch.cuda.stream(self.side2):     # runs a group's collectives in order)
+                if c.analyzer:
+                    with torch.cuda.stream(self.side2):
                         self._analyzer_series(mark)
-        for s in (self.main, self.side, self.side2):
+        for s in (self.main, self.side, self.side2, self.side3):
             caller.wait_stream(s)
         self.ctx.bind_stream()
 
@@ -780,10 +804,12 @@ class Pipeline:
             pad[:j1 - j0] = t[j0:j1]
             pads.append(pad)
         got = self.comm.all_gather_packed(pads)
-        for k, g in zip(keys, got):
-            for q in range(self.W):
-                a, b = _even(self.an_nd, self.W, q)
-                an[k][a:b] = g[q, :b - a]
+        if self._an_rows is None:           # gathered row (rank q, j) of every analyzer date
+            self._an_rows = _share_rows([_even(self.an_nd, self.W, q) for q in range(self.W)], n,
+                                        an["ic"].device)
+        for k, g in zip(keys, got):         # one gather per key, not one copy per rank
+            torch.index_select(g.reshape((-1,) + tuple(g.shape[2:])), 0, self._an_rows,
+                               out=an[k][:self.an_nd])
 
     def _place(self, dst, gathered, rows=None):
         """Scatter per-rank shard columns ([W][rows][wide]) into a full-width plane.  Rank q's
@@ -835,9 +861,7 @@ class Pipeline:
                 own = torch.cat([own, pad])
             owns.append(own)
         if self._reb_rows is None:          # gathered row (rank q, i) of every rebalance date
-            self._reb_rows = torch.as_tensor(
-                np.concatenate([q * self.nr_max + np.arange(b - a) for q, (a, b)
-                                in enumerate(self.rrange)]).astype(np.int64), device=x["k"].device)
+            self._reb_rows = _share_rows(self.rrange, self.nr_max, x["k"].device)
         for k, gath in zip(x.keys(), self.comm.all_gather_packed(owns)):
             if self.nd > 0:                 # one gather per key, not one copy per rank
                 torch.index_select(gath.reshape((-1,) + tuple(gath.shape[2:])), 0,
@@ -851,12 +875,11 @@ class Pipeline:
         sub = recv.view(W, self.fnd, pef).transpose(0, 1).contiguous()     # [fnd][W][part]
         h = self.ctx.bind_stream()
         self._fm_solve(h, sub)
-        bg, ng, kg = self.comm.all_gather_packed([self.fm_beta_own, self.fm_nobs_own,
-                                                  self.fm_rank_own])
-        for q, (lo, hi) in enumerate(self.fdr):
-            self.fm_beta[lo:hi] = bg[q, :hi - lo]
-            self.fm_nobs[lo:hi] = ng[q, :hi - lo]
-            self.fm_rank[lo:hi] = kg[q, :hi - lo]
+        got = self.comm.all_gather_packed([self.fm_beta_own, self.fm_nobs_own, self.fm_rank_own])
+        if self._fm_rows is None:           # gathered row (rank q, i) of every FM date
+            self._fm_rows = _share_rows(self.fdr, self.fnd_max, self.fm_beta.device)
+        for g, dst in zip(got, (self.fm_beta, self.fm_nobs, self.fm_rank)):
+            torch.index_select(g.reshape((-1,) + tuple(g.shape[2:])), 0, self._fm_rows, out=dst)
         self._fm_stats(self.ctx.bind_stream())
 
     def _fm_stats(self, h):

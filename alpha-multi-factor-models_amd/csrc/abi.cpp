@@ -23,6 +23,26 @@ hipError_t afm_lds_opt_in(const afm_ctx* ctx, const void* kernel, int bytes) {
 
 int afm_ctx_cus(afm_ctx* ctx) { return ctx->ncu; }
 
+void* afm_ctx_scratch(afm_ctx* ctx, int slot, size_t bytes, hipError_t* err) {
+    *err = hipSuccess;
+    if (bytes == 0) bytes = 1;
+    std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+    auto& e = ctx->scratch[std::make_pair(slot, ctx->stream)];
+    if (e.first && e.second >= bytes) return e.first;
+    if (e.first) {                       // the stream's earlier calls may still use it
+        if ((*err = hipStreamSynchronize(ctx->stream)) != hipSuccess) return nullptr;
+        if ((*err = hipFree(e.first)) != hipSuccess) return nullptr;
+        e.first = nullptr;
+        e.second = 0;
+    }
+    const size_t want = bytes + bytes / 4;   // headroom: a slightly larger call reuses it
+    void* p = nullptr;
+    if ((*err = hipMalloc(&p, want)) != hipSuccess) return nullptr;
+    e.first = p;
+    e.second = want;
+    return p;
+}
+
 extern "C" {
 
 const char* afm_last_error(void) { return g_last_error.c_str(); }
@@ -120,6 +140,12 @@ int afm_ctx_destroy(afm_ctx* ctx) {
         return AFM_E_STATE;
     }
     ctx->magic = 0;
+    if (!ctx->scratch.empty()) {
+        const afm_device_guard dg(ctx->device);
+        (void)hipDeviceSynchronize();
+        for (auto& kv : ctx->scratch)
+            if (kv.second.first) (void)hipFree(kv.second.first);
+    }
     delete ctx;
     return AFM_OK;
 }

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <map>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -46,7 +47,28 @@ struct afm_ctx {
     // compute units of the device (hipDeviceAttributeMultiprocessorCount), read once by
     // afm_ctx_create: launch shapes that fill the chip are chosen from it
     int ncu = 256;
+    // scratch buffers of the entry points, one per (slot, stream), kept across calls
+    // (afm_ctx_scratch); freed by afm_ctx_destroy
+    std::map<std::pair<int, hipStream_t>, std::pair<void*, size_t>> scratch;
+    std::mutex scratch_mu;
 };
+
+// Scratch of an entry point: slot `slot` of the context on its current stream, at least `bytes`.
+// Reused call after call in stream order (the work of one stream runs in order, so a call's
+// kernels never overlap the previous call's on the same buffer); it grows only when a call needs
+// more (the stream is drained first, then a new buffer).  Round 6: the per-call
+// hipMallocAsync / hipFreeAsync pairs it replaces BLOCKED the host (measured with
+// tools/host_probe.py on MI355X: 13.7 ms inside afm_pnl_scan_f64 and 6.2 ms inside
+// afm_factors_f64 per 31-ms step), which serialised the host with the GPU every step.
+enum afm_scratch_slot {
+    AFM_SCRATCH_FACTOR_PARTS = 0,   // factor kernel mask partials (afm_factors_f64 / slab calls)
+    AFM_SCRATCH_PNL = 1,            // afm_pnl_scan_f64 turnover records
+    AFM_SCRATCH_BOOT = 2,           // afm_bootstrap_pnl_f64 path records
+    AFM_SCRATCH_REB_HIST = 3,       // afm_rebalance_f64 member-major history (books > 32)
+    AFM_SCRATCH_REB_SCR = 4,        // afm_rebalance_f64 window staging
+    AFM_SCRATCH_POOL = 5,           // pooled-moment tree levels (xsreg.hip)
+};
+void* afm_ctx_scratch(afm_ctx* ctx, int slot, size_t bytes, hipError_t* err);
 
 // the context device's compute-unit count (read when the context was created)
 int afm_ctx_cus(afm_ctx* ctx);

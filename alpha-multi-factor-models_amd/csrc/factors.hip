@@ -2315,9 +2315,12 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
     const int code = factor_types(ctx, nblk);
     const int types = code_types(code), nparts = code_parts(code);
     uint64_t* part = ext_part;        // per-job-wave mask partials (masks_kernel ORs them)
-    if (!ext_part)
-        AFM_HIP(hipMallocAsync((void**)&part, sizeof(uint64_t) * 2 * nparts * nwords * lda,
-                               ctx->stream));
+    if (!ext_part) {
+        hipError_t e;
+        part = (uint64_t*)afm_ctx_scratch(ctx, AFM_SCRATCH_FACTOR_PARTS,
+                                          sizeof(uint64_t) * 2 * nparts * nwords * lda, &e);
+        AFM_HIP(e);
+    }
     afm::Args a;
     a.T = T;
     a.lda = lda;
@@ -2364,10 +2367,7 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
             afm_set_error("factor kernel: factor_split is not a split of the job sets");
             rc = AFM_E_ARG;
     }
-    if (rc != AFM_OK) {
-        if (!ext_part) (void)hipFreeAsync(part, ctx->stream);
-        return rc;
-    }
+    if (rc != AFM_OK) return rc;
     AFM_HIP(hipGetLastError());
     if (ext_part) return AFM_OK;      // (labels: this entry takes none, see the header)
     const int64_t nw = nwords * lda;
@@ -2384,7 +2384,6 @@ static int factors_slab(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda, int64_t
                            (double*)a.out + 97 * a.plane);
         AFM_HIP(hipGetLastError());
     }
-    AFM_HIP(hipFreeAsync(part, ctx->stream));
     return AFM_OK;
 }
 

@@ -2353,17 +2353,22 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
         hT0 = window > 0 ? 0 : h_t0;
         hTn = window > 0 ? T : (h_t1 > h_t0 ? h_t1 - h_t0 : 0);
         if (hTn > 0) {
-            AFM_HIP(hipMallocAsync((void**)&histT, sizeof(double) * (size_t)lda * hTn,
-                                   ctx->stream));
+            hipError_t e;
+            histT = (double*)afm_ctx_scratch(ctx, AFM_SCRATCH_REB_HIST,
+                                             sizeof(double) * (size_t)lda * hTn, &e);
+            AFM_HIP(e);
             hipLaunchKernelGGL(hist_transpose_kernel, dim3((unsigned)((hTn + 63) / 64),
                                                            (unsigned)(lda / 64)),
                                dim3(256), 0, ctx->stream, lda, A, hist, hist_bits, hT0, hTn, histT,
                                dates, nd, window);
             AFM_HIP(hipGetLastError());
         }
-    } else if (top_n * (top_n + 1) / 2 > kT && hrows > 0)
-        AFM_HIP(hipMallocAsync((void**)&hscr, sizeof(double) * (size_t)nd * 2 * top_n * hrows,
-                               ctx->stream));
+    } else if (top_n * (top_n + 1) / 2 > kT && hrows > 0) {
+        hipError_t e;
+        hscr = (double*)afm_ctx_scratch(ctx, AFM_SCRATCH_REB_SCR,
+                                        sizeof(double) * (size_t)nd * 2 * top_n * hrows, &e);
+        AFM_HIP(e);
+    }
     RebArgs r{T, lda, A, dates, nd, pred, trad_bits, hist, hist_bits, h_t0, h_t1, window, close,
               tmr, top_n, lo, hi, hscr, histT, hT0, hTn, hrows, 0, nullptr, k_out, books, weights,
               sums, upos, usize, status};
@@ -2391,8 +2396,6 @@ extern "C" int afm_rebalance_f64(afm_ctx* ctx, int64_t T, int64_t A, int64_t lda
                 acc[1] * f, acc[4] * f, acc[2] * f, acc[5] * f, acc[6] / (nd * 2), acc[3] * f);
         AFM_HIP(hipFree(r.stamps));
     }
-    if (hscr) AFM_HIP(hipFreeAsync(hscr, ctx->stream));
-    if (histT) AFM_HIP(hipFreeAsync(histT, ctx->stream));
     return rc;
 }
 
@@ -2404,10 +2407,11 @@ extern "C" int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out,
     AFM_CHECK_ARG(k_out && books && sums && upos && usize && value && turnover && long_ret &&
                       short_ret, "null buffer");
     if (nd <= 0) return AFM_OK;
-    int32_t* work = nullptr;
     AFM_CHECK_ARG(nd <= 0x7fffffff, "nd too large for one launch");
-    AFM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * ((size_t)nd * (kRec + 2) + 1),
-                           ctx->stream));
+    hipError_t e;
+    int32_t* work = (int32_t*)afm_ctx_scratch(ctx, AFM_SCRATCH_PNL,
+                                              sizeof(int32_t) * ((size_t)nd * (kRec + 2) + 1), &e);
+    AFM_HIP(e);
     int32_t* rec = work;
     int32_t* rlen = work + nd * kRec;
     AFM_HIP(launch_turnover_terms(ctx, nd, k_out, books, upos, usize, rec, rlen, nullptr, nd,
@@ -2416,7 +2420,6 @@ extern "C" int afm_pnl_scan_f64(afm_ctx* ctx, int64_t nd, const int32_t* k_out,
                        nd, sums, rec, rlen, v0,
                        rate, value, turnover, long_ret, short_ret, (const int32_t*)nullptr);
     AFM_HIP(hipGetLastError());
-    AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;
 }
 
@@ -2453,8 +2456,9 @@ extern "C" int afm_bootstrap_pnl_f64(afm_ctx* ctx, int64_t lda, const int32_t* d
     // rest [n + 1]
     const size_t b_pb = sizeof(uint64_t) * nd * nw, b_up = sizeof(int32_t) * n * 4 * kMaxK,
                  b_us = sizeof(int64_t) * n * 2, b_rec = sizeof(int32_t) * (n * (kRec + 2) + 1);
-    char* work = nullptr;
-    AFM_HIP(hipMallocAsync((void**)&work, b_pb + b_up + b_us + b_rec, ctx->stream));
+    hipError_t e;
+    char* work = (char*)afm_ctx_scratch(ctx, AFM_SCRATCH_BOOT, b_pb + b_up + b_us + b_rec, &e);
+    AFM_HIP(e);
     uint64_t* pbits = (uint64_t*)work;
     int64_t* usize = (int64_t*)(work + b_pb);
     int32_t* upos = (int32_t*)(work + b_pb + b_us);
@@ -2472,6 +2476,5 @@ extern "C" int afm_bootstrap_pnl_f64(afm_ctx* ctx, int64_t lda, const int32_t* d
                        dim3(128), 0, ctx->stream, steps,
                        sums, rec, rlen, v0, rate, value, turnover, long_ret, short_ret, path);
     AFM_HIP(hipGetLastError());
-    AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;
 }

@@ -1087,8 +1087,10 @@ static int pool_tree(afm_ctx* ctx, const double* gram, const double* shift, int 
     const int64_t nb0 = blocks(nseg, pool_level_per(level0));
     double* work = nullptr;
     if (nb0 > 1) {
-        AFM_HIP(hipMallocAsync((void**)&work, sizeof(double) * 2 * nb0 * (p2 * p2 + p2),
-                               ctx->stream));
+        hipError_t e;
+        work = (double*)afm_ctx_scratch(ctx, AFM_SCRATCH_POOL,
+                                        sizeof(double) * 2 * nb0 * (p2 * p2 + p2), &e);
+        AFM_HIP(e);
     }
     const double* ig = gram;
     const double* is = shift;
@@ -1106,7 +1108,6 @@ static int pool_tree(afm_ctx* ctx, const double* gram, const double* shift, int 
         is = os;
         n = nb;
     }
-    if (work) AFM_HIP(hipFreeAsync(work, ctx->stream));
     return AFM_OK;
 }
 

@@ -23,14 +23,14 @@ for step in "$@"; do
       tail -1 $o/smoke.log ;;
     bench)
       timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-variants --no-configs > $o/bench.json 2> $o/bench.err || { tail -5 $o/bench.err; exit 1; }
-      python3 -c "import json; d=json.load(open('$o/bench.json')); print(d['ms_per_step'], d['value'], {k: round(v, 2) for k, v in d['stage_ms'].items()}); print('roof', d['roofline']['frac'], d['roofline_next']['frac'])" ;;
+      python3 -c "import json; d=json.load(open('$o/bench.json')); print(d['ms_per_step'], d['value'], 'host', d.get('host_issue_ms_per_step'), {k: round(v, 2) for k, v in d['stage_ms'].items()}); print('roof', d['roofline']['frac'], d['roofline_next']['frac'])" ;;
     full)
       timeout -k 10 900 python -u bench.py > $o/full.json 2> $o/full.err || { tail -5 $o/full.err; exit 1; }
       python3 -c "import json; d=json.load(open('$o/full.json')); print(d['ms_per_step'], d['value'], d['stage_ms']); print('roof', d['roofline']['frac'], d['roofline_next']['frac']); [print(k, json.dumps(d[k])[:300]) for k in ('top_n_100', 'dense_lasso', 'config_b', 'config_d', 'config_e', 'cpu_baseline')]" ;;
     emu)
       for w in 8 4 2; do
         timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --emulate-world $w > $o/emu$w.json 2> $o/emu$w.err || { tail -5 $o/emu$w.err; exit 1; }
-        python3 -c "import json; d=json.loads(open('$o/emu$w.json').read().strip().splitlines()[-1]); print('emu$w', d['ms_per_step'], {k: round(v, 2) for k, v in d['stage_ms'].items()})"
+        python3 -c "import json; d=json.loads(open('$o/emu$w.json').read().strip().splitlines()[-1]); print('emu$w', d['ms_per_step'], 'host', d.get('host_issue_ms_per_step'), {k: round(v, 2) for k, v in d['stage_ms'].items()})"
       done ;;
     prof) bash tools/gpu_prof.sh $TAG || exit 1 ;;
     pmc) bash tools/gpu_pmc.sh $TAG || exit 1 ;;

@@ -1,11 +1,13 @@
 """Per-kernel timeline of the last bench step from a rocprofv3 kernel trace (start offset from the
-step's factor kernel, duration, stream).  Usage: python tools/trace_step.py run_kernel_trace.csv"""
+step's first factor kernel, duration, stream).
+Usage: python tools/trace_step.py run_kernel_trace.csv [factor launches per step (slabs), default 1]"""
 import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 fk = [r for r in rows if "factor_panel" in r["Kernel_Name"]]
-t0 = int(fk[-1]["Start_Timestamp"])
+per = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+t0 = int(fk[-per]["Start_Timestamp"])
 for r in rows:
     s = int(r["Start_Timestamp"])
     if s >= t0 - 2_000_000:
