@@ -129,6 +129,11 @@ class PipelineConfig:
     # KKT:294-296) on a side stream as soon as the all_df rows exist, beside the z statistics,
     # instead of at the head of the analyzer stream in the tail
     early_fwd: bool = True
+    # reb_split -- N > 1: each rank runs the rebalance of its share of the dates (+ one neighbour
+    # per side) and one packed all-gather assembles the books; False: every rank runs every date
+    # (the rebalance is latency-bound -- one workgroup per (date, side) -- so a rank's share is
+    # not much shorter than all of it) and there is no exchange
+    reb_split: bool = True
 
 
 @dataclass
@@ -326,13 +331,15 @@ class Pipeline:
         self.reb = reb_buffers(nd)
         # rebalance dates of this rank (+ one neighbour per side: the turnover alignment needs the
         # adjacent dates' prediction sets)
-        self.rrange = [_even(nd, W, q) for q in range(W)]
-        i0, i1 = self.rrange[rk]
+        self.reb_split = W > 1 and c.reb_split
+        Wr = W if self.reb_split else 1
+        self.rrange = [_even(nd, Wr, q) for q in range(Wr)]
+        i0, i1 = self.rrange[rk if self.reb_split else 0]
         self.i0, self.i1 = i0, i1
-        self.e0, self.e1 = (max(i0 - 1, 0), min(i1 + 1, nd)) if W > 1 else (0, nd)
+        self.e0, self.e1 = (max(i0 - 1, 0), min(i1 + 1, nd)) if self.reb_split else (0, nd)
         self.rd_ext = torch.from_numpy(rd[self.e0:self.e1].copy()).to(dev)
         self.rdates = torch.from_numpy(rd).to(dev)
-        self.reb_ext = self.reb if W == 1 else reb_buffers(self.e1 - self.e0)
+        self.reb_ext = reb_buffers(self.e1 - self.e0) if self.reb_split else self.reb
         self.nr_max = max(b - a for a, b in self.rrange)
         self._reb_rows = self._fm_rows = self._an_rows = None
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
@@ -755,7 +762,7 @@ class Pipeline:
                                         P(full.close), P(self.tmr), c.top_n, c.lo, c.hi,
                                         P(x["k"]), P(x["books"]), P(x["weights"]), P(x["sums"]),
                                         P(x["upos"]), P(x["usize"]), P(x["status"])), "rebalance")
-            if W > 1:
+            if self.reb_split:
                 self._gather_rebalance()
                 h = self.ctx.bind_stream()
             mark("rebalance", 1)

@@ -48,6 +48,9 @@ def log(*a):
 # per-launch HBM bytes from the latest PMC passes (tools/prof_counters.sh -> tools/pmc_traffic.py;
 # FETCH_SIZE x2 and KiB corrections of MI355X_MICROARCH.md applied there)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r5_w_pmc_traffic.json")
+# config D (the time-slab factor build): HBM bytes of one whole pass, every slab launch of the
+# factor / masks / label kernels (tools/gpu_pmc_config_d.sh -> tools/pmc_pass.py)
+PMC_CONFIG_D = os.path.join(ROOT, "profiles", "r6_pmc_config_d.json")
 ROOF_KERNELS = {"factors": ("factor_panel_kernel", "masks_kernel", "labels_kernel"),
                 "factors_nolabels": ("factor_panel_kernel", "masks_kernel"),
                 "xs_gram": ("zgram_kernel<7, 1, true>",)}
@@ -217,6 +220,14 @@ def config_d_line(seed: int, reps: int) -> dict:
     ms = ev[0].elapsed_time(ev[1]) / reps
     byts = FACTOR_BYTES_PER_AD * bars
     gbs = byts / (ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        with open(PMC_CONFIG_D) as f:
+            pd = json.load(f)
+        if pd.get("workload") == [A, T]:
+            traffic = round(pd["hbm_bytes_per_pass"] / 1e9, 1)
+    except (OSError, ValueError, KeyError):
+        pass
     del g
     torch.cuda.empty_cache()
     return {"what": f"config D (BASELINE configs[3]): {A} assets x {T} one-minute bars, 98 "
@@ -224,7 +235,10 @@ def config_d_line(seed: int, reps: int) -> dict:
             "reps": reps, "ms_per_pass": round(ms, 2), "asset_bars": bars,
             "value": round(bars / (ms * 1e-3), 1), "unit": "asset-bars/s",
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "traffic_unit": "GB per pass (PMC FETCH_SIZE x2 + WRITE_SIZE, every "
+                                         "slab launch)",
                          "kernel": "factor_panel_kernel (+ masks, label planes) per slab",
                          "algorithmic_GB": round(byts / 1e9, 1),
                          "bytes_per_unit": FACTOR_BYTES_PER_AD}}
@@ -410,6 +424,9 @@ def main():
                     help="time what ONE rank of an N-GPU job computes, on one GPU (collectives "
                          "replaced by local copies, afm.sharded.EmulatedComm): a per-rank proxy, "
                          "not a result of the job")
+    ap.add_argument("--reb-split", type=int, default=None,
+                    help="PipelineConfig.reb_split (N > 1: 1 = rebalance dates split over the "
+                         "ranks + all-gather, 0 = every rank all dates)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the config B / D / E lines (N = 1 only)")
@@ -466,6 +483,8 @@ def main():
         place["zstats_slabs"] = args.zstats_slabs
     if args.fm_grid is not None:
         place["fm_grid"] = args.fm_grid
+    if args.reb_split is not None:
+        place["reb_split"] = bool(args.reb_split)
     for k in ("train_end", "valid_end", "window"):
         if getattr(args, k) is not None:
             place[k] = getattr(args, k)

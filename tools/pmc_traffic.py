@@ -19,15 +19,7 @@ import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_summary import short  # noqa: E402
-
-
-def templated(name):
-    """short() plus the template arguments: zgram_kernel<7, 1, true> and zgram_kernel<2, 0,
-    false> are different kernels with different traffic."""
-    k = short(name)
-    m = re.search(re.escape(k) + r"(<[^()]*?>)\(", name)
-    return k + m.group(1) if m else k
+from pmc_summary import short, templated  # noqa: E402
 
 
 def per_launch(path, counter):
