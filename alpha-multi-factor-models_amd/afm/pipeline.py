@@ -400,8 +400,12 @@ class Pipeline:
             self.side = torch.cuda.Stream(device=dev, priority=0)
         self.side2 = torch.cuda.Stream(device=dev, priority=0)
         # N > 1: the sequential PnL scan on its own stream, beside the FM exchange / solve and the
-        # analyzer's gather + series that follow the rebalance (they no longer wait for it)
-        self.side3 = torch.cuda.Stream(device=dev, priority=-8 if c.main_priority else 0)
+        # analyzer's gather + series that follow the rebalance (they no longer wait for it).  One
+        # GPU creates no fourth stream: HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues
+        # in creation order, and a stream that shares a queue waits behind the other's kernels
+        self.side3 = (torch.cuda.Stream(device=dev, priority=-8 if c.main_priority else 0)
+                      if W > 1 else self.main)
+        self.streams = (self.main, self.side, self.side2) + ((self.side3,) if W > 1 else ())
         self.labels_done = torch.cuda.Event()
         self.fwd_early = False
         # early z statistics: the first slab ends at the first 64-date boundary past the train
@@ -617,7 +621,7 @@ class Pipeline:
         T, lda_r, p, W, nch = self.T, self.lda_r, self.p, self.W, self.nch
         full = self.full
         caller = torch.cuda.current_stream(full.device)
-        for s in (self.main, self.side, self.side2, self.side3):
+        for s in self.streams:
             s.wait_stream(caller)
 
         def mark(stage, which):
@@ -793,7 +797,7 @@ class Pipeline:
                 if c.analyzer:
                     with torch.cuda.stream(self.side2):
                         self._analyzer_series(mark)
-        for s in (self.main, self.side, self.side2, self.side3):
+        for s in self.streams:
             caller.wait_stream(s)
         self.ctx.bind_stream()
 

@@ -170,7 +170,7 @@ def test_shard_geometry():
 SPLIT = dict(train_end="2001-06-29", valid_end="2001-12-31", window=120)
 
 
-def _sharded_worker(rank, world, port, outdir, A, T):
+def _sharded_worker(rank, world, port, outdir, A, T, reb_split=True):
     import torch
     _init(rank, world, port)
     import afm
@@ -179,7 +179,7 @@ def _sharded_worker(rank, world, port, outdir, A, T):
     from afm.synthetic import make_panel
     torch.cuda.set_device(0)
     grid = afm.PanelGrid.from_panel(make_panel(A, T, seed=11, tradable_p=0.9))
-    sp = ShardedPipeline(grid, Comm(), PipelineConfig(**SPLIT))
+    sp = ShardedPipeline(grid, Comm(), PipelineConfig(**SPLIT, reb_split=reb_split))
     sp.step()
     sp.step()
     torch.cuda.synchronize()
@@ -200,8 +200,9 @@ def _sharded_worker(rank, world, port, outdir, A, T):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,A,T", [(2, 300, 700), (4, 300, 700), (8, 1000, 640)])
-def test_sharded_ranks_bit_identical_to_single(tmp_path, world, A, T):
+@pytest.mark.parametrize("world,A,T,reb_split", [(2, 300, 700, True), (4, 300, 700, True),
+                                                 (8, 1000, 640, True), (2, 300, 700, False)])
+def test_sharded_ranks_bit_identical_to_single(tmp_path, world, A, T, reb_split):
     """N ranks (gloo, sharing cuda:0) run the whole step: the pooled Gram, Lasso, predictions,
     FM betas, books, weights, PnL and IC are BIT-identical to the one-device step; so are the
     config-E bootstrap paths sharded over the ranks.
@@ -212,14 +213,16 @@ def test_sharded_ranks_bit_identical_to_single(tmp_path, world, A, T):
     8-block split (rank 7 a short one of 104 assets), runs the small-grid factor launch on its
     2-block shard (the 30-set partition PartS, code 110) with the z statistics streamed slab by
     slab behind it, owns 1/8 of the FM dates (the 8-owner all_to_all) and of the rebalance
-    dates.  (The 15-set PartC splits are covered by test_factors_gpu.py.)"""
+    dates.  (The 15-set PartC splits are covered by test_factors_gpu.py.)  reb_split False: every
+    rank runs the rebalance of every date (PipelineConfig.reb_split), no rebalance exchange."""
     import torch
     import torch.multiprocessing as mp
     import afm
     from afm.pipeline import Pipeline, PipelineConfig
     from afm.synthetic import make_panel
     port = _free_port()
-    mp.spawn(_sharded_worker, args=(world, port, str(tmp_path), A, T), nprocs=world, join=True)
+    mp.spawn(_sharded_worker, args=(world, port, str(tmp_path), A, T, reb_split), nprocs=world,
+             join=True)
     s = np.load(tmp_path / "sharded.npz")
     grid = afm.PanelGrid.from_panel(make_panel(A, T, seed=11, tradable_p=0.9))
     pipe = Pipeline(grid, PipelineConfig(**SPLIT))
