@@ -36,6 +36,15 @@ def _init(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
+def _done():
+    """Leave the group cleanly: every rank passed the last barrier, then the process group is
+    destroyed before the process exits (a gloo rank that exits with its group alive can abort a
+    peer still closing its connections)."""
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def test_block_ranges_cover_and_align():
     from afm.sharded import block_range, even_range
     for n in (1, 63, 64, 65, 5040, 10000):
@@ -77,6 +86,7 @@ def _comm_worker(rank, world, port, outdir):
         assert int(gc[q, 0]) == q
     cm.barrier()
     open(os.path.join(outdir, f"ok{rank}"), "w").write("ok")
+    _done()
 
 
 @pytest.mark.parametrize("world", [2, 8])
@@ -115,6 +125,7 @@ def _tree_worker(rank, world, port, outdir):
     assert np.array_equal(total, tree_sum(leaves))
     cm.barrier()
     open(os.path.join(outdir, f"tree{rank}"), "w").write("ok")
+    _done()
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
@@ -142,6 +153,7 @@ def _paths_worker(rank, world, port, outdir):
     # gloo aborts a peer whose connection closes mid-transfer)
     cm.barrier()
     (Path(outdir) / f"paths{rank}").write_text("ok")
+    _done()
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
@@ -197,6 +209,7 @@ def _sharded_worker(rank, world, port, outdir, A, T, reb_split=True):
                  w=sp.reb["weights"].cpu().numpy(), value=sp.pnl["value"].cpu().numpy(),
                  ic=sp.an["ic"].cpu().numpy())
     Comm().barrier()
+    _done()
 
 
 @pytest.mark.gpu
