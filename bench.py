@@ -47,7 +47,7 @@ def log(*a):
 
 # per-launch HBM bytes from the latest PMC passes (tools/prof_counters.sh -> tools/pmc_traffic.py;
 # FETCH_SIZE x2 and KiB corrections of MI355X_MICROARCH.md applied there)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r5_w_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r6z_pmc_traffic.json")
 # config D (the time-slab factor build): HBM bytes of one whole pass, every slab launch of the
 # factor / masks / label kernels (tools/gpu_pmc_config_d.sh -> tools/pmc_pass.py)
 PMC_CONFIG_D = os.path.join(ROOT, "profiles", "r6_pmc_config_d.json")
