@@ -77,6 +77,9 @@ STAGES = ("factors", "zstats", "xs_gram", "lasso", "predict", "rebalance", "pnl"
           "analyzer")
 PIPELINE_STAGES = STAGES
 EXCHANGE_STAGES = STAGES + ("exchange",)
+# optional step() events around single launches (bench.py's rooflines): the one-pass factor call
+# (factor_panel_kernel + masks_kernel) and the pooled Gram's partial kernel (zgram_kernel<7, 1>)
+KERNEL_MARKS = ("k_factor", "k_gram")
 
 
 @dataclass
@@ -445,7 +448,7 @@ class Pipeline:
         return int(self.g.valid.sum().item())
 
     # ------------------------------------------------------------------------------------------
-    def _pooled_blocks(self, h, t0, nt):
+    def _pooled_blocks(self, h, t0, nt, mark=None):
         """This shard's pooled-Gram block results (rows of the dates [t0, t0 + nt)): row-block x
         chunk partials, then the tree -- the chunks of a row-block (32, then 2), the row-blocks
         of an asset block -> pool_blk[0:nblk_r]."""
@@ -454,9 +457,13 @@ class Pipeline:
         self.pool_blk.zero_()
         if self.nrb == 0:
             return
+        if mark is not None:
+            mark("k_gram", 0)
         chk(L.afm_zpool_f64(h, P(self.out), T * lda, lda, P(self.feat), None, p, TARGET,
                             P(self.zs), p, P(self.zrows), t0, nt, 0, self.nrb, self.A_r,
                             N_CHUNKS, P(self.pool_part), 0), "zpool")
+        if mark is not None:
+            mark("k_gram", 1)
         c1, c2 = CHUNK_TREE
         chk(L.afm_gram_tree_f64(h, p, P(self.pool_part), self.nrb * N_CHUNKS, c1, 0,
                                 P(self.pool_c1)), "tree chunks")
@@ -641,10 +648,12 @@ class Pipeline:
                 self._factors_early(h, lab_side, mark)
                 h = self.ctx.bind_stream()
             elif self.A_r > 0:
+                mark("k_factor", 0)
                 chk(L.afm_factors_f64(h, T, self.A_r, lda_r, P(g.close), P(g.volume),
                                       None if lab_side else P(g.ret1d),
                                       None if lab_side else P(g.excess), P(g.vbits), P(self.out),
                                       P(self.nanfree), P(self.finite)), "factors")
+                mark("k_factor", 1)
                 if lab_side:
                     with torch.cuda.stream(self.side2):
                         h2 = self.ctx.bind_stream()
@@ -689,7 +698,7 @@ class Pipeline:
                     self.labels_done.record(self.side2)
                 h = self.ctx.bind_stream()
             mark("xs_gram", 0)
-            self._pooled_blocks(h, 0, sp.v1)                        # train + valid rows
+            self._pooled_blocks(h, 0, sp.v1, mark)                  # train + valid rows
             if sp.dup:                                              # train_end counted twice
                 self._te_subtree(h, sp.tr1 - 1)
             if W > 1:

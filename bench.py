@@ -142,25 +142,47 @@ def cpu_port(seed: int, assets: int = 150, days: int = 2520):
                       f"asset-days: " + ", ".join(f"{k} {v:.2f}s" for k, v in tm.items())}
 
 
-def rooflines(pipe, stage_ms: dict, n_ad_local: int, world: int, assets: int, days: int):
+def kernel_times(evs: list) -> dict:
+    """Mean device time (ms) of each KERNEL_MARKS pair the timed steps recorded (the one-pass
+    factor call and the pooled Gram's partial kernel, on the main stream); marks a step path
+    does not record (time slabs, the early z statistics) are left out."""
+    from afm.pipeline import KERNEL_MARKS
+    out = {}
+    for k in KERNEL_MARKS:
+        try:
+            out[k] = sum(e[k][0].elapsed_time(e[k][1]) for e in evs) / len(evs)
+        except (KeyError, RuntimeError, ValueError):   # a pair the path never recorded
+            pass
+    return out
+
+
+def rooflines(pipe, stage_ms: dict, n_ad_local: int, world: int, assets: int, days: int,
+              kms: dict | None = None):
     """The factor kernel (HBM) and pooled Gram (fp64 MFMA) roofline objects of one timed
-    Pipeline, ranked by their stage's device time (dominant first)."""
+    Pipeline, ranked by their stage's device time (dominant first).  ``achieved`` divides by the
+    kernel's own event time when the step recorded it (``kernel_times``), else by its stage's."""
+    kms = kms or {}
     labels_in = world == 1 and pipe.labels_in_factor_stage
     fac_bytes = FACTOR_BYTES_PER_AD if labels_in else FACTOR_BYTES_NO_LABELS
-    fac_gbs = fac_bytes * n_ad_local / (stage_ms["factors"] * 1e-3) / 1e9
+    fac_ms = kms.get("k_factor", stage_ms["factors"])
+    gram_ms = kms.get("k_gram", stage_ms["xs_gram"])
+    fac_gbs = fac_bytes * n_ad_local / (fac_ms * 1e-3) / 1e9
     p2 = pipe.p2
     rows_tv = float(pipe.pool_g[0, 0, 0].item())           # pooled rows (n of the Gram)
     if pipe.sp.dup:
         rows_tv -= float(pipe.te_gram[0, 0, 0].item())       # the duplicate is not recomputed
     rows_tv /= (world if world > 1 else 1)
-    gram_tfs = rows_tv * p2 * (p2 + 1) / (stage_ms["xs_gram"] * 1e-3) / 1e12
+    gram_tfs = rows_tv * p2 * (p2 + 1) / (gram_ms * 1e-3) / 1e12
     single = world == 1
     fac = {"bound": "hbm", "achieved": round(fac_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(fac_gbs / HBM_PEAK_GBS, 4),
            "traffic": None,
-           "kernel": "factor_panel_kernel (+ masks, row-bit kernels%s)" % (
-               ", label planes" if labels_in else "; label planes on a side stream"),
-           "kernel_ms": round(stage_ms["factors"], 3),
+           "kernel": ("factor_panel_kernel + masks_kernel (one launch%s)" % (
+               ", label planes inside" if labels_in else "; label planes on a side stream")
+               if "k_factor" in kms else
+               "factor_panel_kernel (+ masks, row-bit kernels%s)" % (
+                   ", label planes" if labels_in else "; label planes on a side stream")),
+           "kernel_ms": round(fac_ms, 3), "stage_ms": round(stage_ms["factors"], 3),
            "algorithmic_GB": round(fac_bytes * n_ad_local / 1e9, 3)}
     tb = (pmc_traffic("factors" if labels_in else "factors_nolabels", assets, days)
           if single else None)
@@ -169,8 +191,11 @@ def rooflines(pipe, stage_ms: dict, n_ad_local: int, world: int, assets: int, da
         fac["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
     gram = {"bound": "mfma", "achieved": round(gram_tfs, 2), "peak": F64_MFMA_PEAK_TFS,
             "unit": "TFLOP/s", "frac": round(gram_tfs / F64_MFMA_PEAK_TFS, 4),
-            "traffic": None, "kernel": "zgram_kernel<7,1> + tree_merge_kernel (pooled train+valid Gram)",
-            "kernel_ms": round(stage_ms["xs_gram"], 3),
+            "traffic": None,
+            "kernel": ("zgram_kernel<7,1> (pooled train+valid Gram partials; the stage adds the "
+                       "tree merges)" if "k_gram" in kms else
+                       "zgram_kernel<7,1> + tree_merge_kernel (pooled train+valid Gram)"),
+            "kernel_ms": round(gram_ms, 3), "stage_ms": round(stage_ms["xs_gram"], 3),
             "algorithmic_GFLOP": round(rows_tv * p2 * (p2 + 1) / 1e9, 3)}
     tg = pmc_traffic("xs_gram", assets, days) if single else None
     if tg is not None:
@@ -317,12 +342,12 @@ def variant_line(grid, cfg, steps: int, warmup: int, what: str, roof=None) -> di
     step, W untimed + K timed steps bracketed by synchronize, per-stage device times."""
     import numpy as np
     import torch
-    from afm.pipeline import PIPELINE_STAGES, Pipeline
+    from afm.pipeline import KERNEL_MARKS, PIPELINE_STAGES, Pipeline
     pipe = Pipeline(grid, cfg)
     for _ in range(warmup):
         pipe.step()
     evs = [{st: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for st in PIPELINE_STAGES} for _ in range(steps)]
+            for st in PIPELINE_STAGES + KERNEL_MARKS} for _ in range(steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
@@ -342,7 +367,7 @@ def variant_line(grid, cfg, steps: int, warmup: int, what: str, roof=None) -> di
     out["weights_at_bounds_frac"] = round(float(((w <= cfg.lo) | (w >= cfg.hi)).mean()), 4)
     if roof is not None:
         out["assets"], out["days"] = roof
-        rl = rooflines(pipe, stage_ms, grid.n_asset_days(), 1, *roof)
+        rl = rooflines(pipe, stage_ms, grid.n_asset_days(), 1, *roof, kms=kernel_times(evs))
         out["roofline"], out["roofline_next"] = rl[0], rl[1]
         out["fm_ms"] = stage_ms["fm"]
         out["ic_mean"] = [round(float(x), 6) for x in s.get("ic_mean", [])]
@@ -517,8 +542,9 @@ def main():
             f"{np.bincount(s['fm_rank'])[-2:]}, k {np.bincount(s['k'])[-2:]}, qp status "
             f"{np.bincount(s['status'])}, mean IC {s.get('ic_mean')}")
 
+    from afm.pipeline import KERNEL_MARKS
     evs = [{st: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for st in stages} for _ in range(args.steps)]
+            for st in stages + KERNEL_MARKS} for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -557,7 +583,8 @@ def main():
         # (HBM: 816 B per asset-day; 784 B without the two label planes, which
         # run on a side stream beside the factor kernel) and the pooled Gram (fp64 MFMA:
         # rows * (p+2)(p+3) flops over the train + valid rows, zpool + tree merges).
-        ranked = rooflines(pipe, stage_ms, n_ad_local, world, args.assets, args.days)
+        ranked = rooflines(pipe, stage_ms, n_ad_local, world, args.assets, args.days,
+                           kernel_times(evs))
         res = {
             "metric": "asset-days/sec, factor build+XS regression+KKT (10k assets x 20y), "
                       "1/2/4/8 GPU",

@@ -71,3 +71,13 @@ def test_bench_self_launch_two_ranks():
     assert d1["config"]["asset_days"] == d2["config"]["asset_days"]
     # the sharded step is bit-identical to the one-device step (tests/test_sharded.py)
     assert d2["final_value"] == d1["final_value"]
+    # one GPU: the rooflines divide by the kernel's own event time where the step path records
+    # it (the pooled Gram's partial kernel always; this small grid builds its factor panel in
+    # time slabs, so the factor roofline keeps its stage time), never more than the stage's
+    roofs = {r["bound"]: r for r in (d1["roofline"], d1["roofline_next"])}
+    for r in roofs.values():
+        assert 0 < r["kernel_ms"] <= r["stage_ms"]
+        assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-2)
+    assert roofs["hbm"]["kernel"].startswith("factor_panel_kernel")
+    assert roofs["mfma"]["kernel"].startswith("zgram_kernel<7,1> (pooled")
+    assert roofs["mfma"]["kernel_ms"] < roofs["mfma"]["stage_ms"]
