@@ -55,13 +55,18 @@ class Comm:
         """Equal-shape all-gather -> tensor [world, *t.shape] on t's device."""
         import torch
         src = self._stage(t.contiguous())
-        out = torch.empty((self.world,) + tuple(src.shape), dtype=src.dtype, device=src.device)
         if self.host:
             parts = [torch.empty_like(src) for _ in range(self.world)]
             self.dist.all_gather(parts, src, group=self.group)
             out = torch.stack(parts)
         else:
-            self.dist.all_gather_into_tensor(out, src, group=self.group)
+            # the ranks' tensors concatenated along dim 0 (the output form every backend takes;
+            # the stacked form is NCCL-only), then viewed [world, *t.shape]
+            flat = src if src.dim() else src.reshape(1)
+            out = torch.empty((self.world * flat.shape[0],) + tuple(flat.shape[1:]),
+                              dtype=src.dtype, device=src.device)
+            self.dist.all_gather_into_tensor(out, flat, group=self.group)
+            out = out.view((self.world,) + tuple(src.shape))
         return out.to(t.device)
 
     def all_gather_packed(self, tensors):

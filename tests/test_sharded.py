@@ -1,7 +1,9 @@
 """Multi-rank path (afm/pipeline.py with a Comm).
 
-CPU (gloo, world size 2 and 4): shard geometry, the Comm collectives the step uses (equal-shape
-all-gather, all_to_all with uneven splits, packed all-gather), and the subtree exchange: a rank's
+CPU (gloo, world size 2 to 8): shard geometry, the Comm collectives the step uses (equal-shape
+all-gather, all_to_all with uneven splits, packed all-gather) on both of Comm's branches -- host
+staging (gloo) and the device-tensor calls a GPU job makes over RCCL (all_gather_into_tensor,
+all_to_all_single), here driven through gloo on CPU tensors -- and the subtree exchange: a rank's
 subtree sum, all-gathered and summed over the same tree, equals the one-process tree bit for bit.
 GPU: 2 and 4 ranks sharing cuda:0 over gloo run the whole step and are BIT-identical to the
 single-device Pipeline (pooled Gram, Lasso, predictions, FM betas, books, weights, PnL, IC).
@@ -64,6 +66,20 @@ def _comm_worker(rank, world, port, outdir):
     from afm.sharded import Comm
     cm = Comm()
     assert cm.host and cm.world == world and cm.rank == rank
+    _check_collectives(cm, rank, world)
+    # the device-tensor branch (RCCL's on a GPU job: all_gather_into_tensor into one
+    # concatenated buffer, all_to_all_single) run through gloo on CPU tensors
+    cm.host = False
+    _check_collectives(cm, rank, world)
+    g0 = cm.all_gather(torch.tensor(float(rank)))            # a 0-d tensor
+    assert g0.shape == (world,) and torch.equal(g0, torch.arange(world, dtype=g0.dtype))
+    cm.barrier()
+    open(os.path.join(outdir, f"ok{rank}"), "w").write("ok")
+    _done()
+
+
+def _check_collectives(cm, rank, world):
+    import torch
     g = cm.all_gather(torch.full((3, 2), float(rank)))
     assert g.shape == (world, 3, 2) and all((g[q] == q).all() for q in range(world))
     # all_to_all with uneven splits: rank r sends q+1+r rows to rank q, row value = 100 r + q
@@ -84,9 +100,6 @@ def _comm_worker(rank, world, port, outdir):
         assert torch.equal(ga[q], torch.arange(6, dtype=torch.int32).view(2, 3) + 10 * q)
         assert torch.equal(gb[q], torch.full((5,), 0.5 + q, dtype=torch.float64))
         assert int(gc[q, 0]) == q
-    cm.barrier()
-    open(os.path.join(outdir, f"ok{rank}"), "w").write("ok")
-    _done()
 
 
 @pytest.mark.parametrize("world", [2, 8])
