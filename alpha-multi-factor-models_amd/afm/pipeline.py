@@ -345,6 +345,7 @@ class Pipeline:
         self.reb_ext = reb_buffers(self.e1 - self.e0) if self.reb_split else self.reb
         self.nr_max = max(b - a for a, b in self.rrange)
         self._reb_rows = self._fm_rows = self._an_rows = None
+        self._send = {}                     # packed send buffers of the exchanges (N > 1)
         self.pnl = {"value": torch.empty(nd + 1, **f64), "turnover": torch.empty(nd, **f64),
                     "long_ret": torch.empty(nd, **f64), "short_ret": torch.empty(nd, **f64)}
         # analyzer on the test sub-grid (64-date aligned, so the bit words line up)
@@ -811,19 +812,25 @@ class Pipeline:
         self.ctx.bind_stream()
 
     # ---- exchanges (N > 1) -------------------------------------------------------------------
+    def _send_buffer(self, key, specs, device):
+        """The persistent packed send buffer of one exchange (made on its first step)."""
+        from .packing import SendBuffer
+        sb = self._send.get(key)
+        if sb is None:
+            sb = self._send[key] = SendBuffer(specs, device)
+        return sb
+
     def _gather_analyzer(self):
         """The per-date analyzer results of every rank's date share -> the full arrays (one
         packed all-gather, shares padded to the largest)."""
         import torch
         an, (j0, j1), n = self.an, self.an_rng, self.an_nmax
         keys = ("ic", "layer_mean", "layer_cnt", "port")
-        pads = []
-        for k in keys:
-            t = an[k]
-            pad = torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-            pad[:j1 - j0] = t[j0:j1]
-            pads.append(pad)
-        got = self.comm.all_gather_packed(pads)
+        sb = self._send_buffer("an", [((n,) + tuple(an[k].shape[1:]), an[k].dtype, 0)
+                                      for k in keys], an["ic"].device)
+        for k, part in zip(keys, sb.parts):          # rows past the share stay zero
+            part[:j1 - j0].copy_(an[k][j0:j1])
+        got = self.comm.all_gather_buffer(sb)
         if self._an_rows is None:           # gathered row (rank q, j) of every analyzer date
             self._an_rows = _share_rows([_even(self.an_nd, self.W, q) for q in range(self.W)], n,
                                         an["ic"].device)
@@ -854,15 +861,15 @@ class Pipeline:
     def _gather_test_planes(self):
         import torch
         s0, wide, A_r = self.sp.s0, self.wide, self.A_r
-        pr = torch.full((self.T - s0, wide), float("nan"), dtype=torch.float64,
-                        device=self.pred_r.device)
-        zb = torch.zeros((self.nch, wide), dtype=torch.int64, device=self.pred_r.device)
-        ab = torch.zeros_like(zb)
+        sb = self._send_buffer("test", [((self.T - s0, wide), torch.float64, float("nan")),
+                                        ((self.nch, wide), torch.int64, 0),
+                                        ((self.nch, wide), torch.int64, 0)], self.pred_r.device)
+        pr, zb, ab = sb.parts                       # columns past A_r keep NaN / 0
         if A_r > 0:
-            pr[:, :A_r] = self.pred_r[s0:, :A_r]
-            zb[:, :A_r] = self.zrows[:, :A_r]
-            ab[:, :A_r] = self.alldf[:, :A_r]
-        gp, gz, ga = self.comm.all_gather_packed([pr, zb, ab])
+            pr[:, :A_r].copy_(self.pred_r[s0:, :A_r])
+            zb[:, :A_r].copy_(self.zrows[:, :A_r])
+            ab[:, :A_r].copy_(self.alldf[:, :A_r])
+        gp, gz, ga = self.comm.all_gather_buffer(sb)
         self._place(self.pred, gp, rows=slice(s0, self.T))
         self._place(self.zrows_full, gz)
         self._place(self.alldf_full, ga)
@@ -872,17 +879,13 @@ class Pipeline:
         x = self.reb_ext
         lo = self.i0 - self.e0
         n_own = self.i1 - self.i0
-        owns = []
-        for k, v in x.items():
-            own = v[lo:lo + n_own]
-            if n_own < self.nr_max:
-                pad = torch.zeros((self.nr_max - n_own,) + tuple(v.shape[1:]), dtype=v.dtype,
-                                  device=v.device)
-                own = torch.cat([own, pad])
-            owns.append(own)
+        sb = self._send_buffer("reb", [((self.nr_max,) + tuple(v.shape[1:]), v.dtype, 0)
+                                       for v in x.values()], x["k"].device)
+        for v, part in zip(x.values(), sb.parts):    # rows past the share stay zero
+            part[:n_own].copy_(v[lo:lo + n_own])
         if self._reb_rows is None:          # gathered row (rank q, i) of every rebalance date
             self._reb_rows = _share_rows(self.rrange, self.nr_max, x["k"].device)
-        for k, gath in zip(x.keys(), self.comm.all_gather_packed(owns)):
+        for k, gath in zip(x.keys(), self.comm.all_gather_buffer(sb)):
             if self.nd > 0:                 # one gather per key, not one copy per rank
                 torch.index_select(gath.reshape((-1,) + tuple(gath.shape[2:])), 0,
                                    self._reb_rows, out=self.reb[k][:self.nd])

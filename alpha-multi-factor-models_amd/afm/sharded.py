@@ -89,6 +89,11 @@ class Comm:
             off += n
         return out
 
+    def all_gather_buffer(self, sb):
+        """ONE all-gather of a ``packing.SendBuffer`` -> its parts as [world, *shape] views."""
+        from .packing import unpack_gathered
+        return unpack_gathered(self.all_gather(sb.buf), sb.layout, self.world)
+
     def all_to_all(self, inp, in_splits, out_splits):
         """all_to_all_single along dim 0 with explicit split sizes (rows)."""
         import torch
@@ -120,6 +125,10 @@ class EmulatedComm:
 
     def all_gather_packed(self, tensors):
         return [self.all_gather(t) for t in tensors]
+
+    def all_gather_buffer(self, sb):
+        from .packing import unpack_gathered
+        return unpack_gathered(self.all_gather(sb.buf), sb.layout, self.world)
 
     def all_to_all(self, inp, in_splits, out_splits):
         import torch

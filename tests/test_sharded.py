@@ -100,6 +100,20 @@ def _check_collectives(cm, rank, world):
         assert torch.equal(ga[q], torch.arange(6, dtype=torch.int32).view(2, 3) + 10 * q)
         assert torch.equal(gb[q], torch.full((5,), 0.5 + q, dtype=torch.float64))
         assert int(gc[q, 0]) == q
+    # the same through a persistent send buffer (afm.packing): typed parts at aligned offsets that
+    # keep their fill where a step does not write, gathered as strided views
+    from afm.packing import SendBuffer
+    sb = SendBuffer([((2, 3), torch.int32, 0), ((5,), torch.float64, float("nan")),
+                     ((1,), torch.int64, 0)], "cpu")
+    sb.parts[0].copy_(a)
+    sb.parts[1][:2] = 0.5 + rank
+    sb.parts[2][0] = rank
+    for step in range(2):                      # reused: the fills survive, the rows are rewritten
+        ha, hb, hc = cm.all_gather_buffer(sb)
+        for q in range(world):
+            assert torch.equal(ha[q], torch.arange(6, dtype=torch.int32).view(2, 3) + 10 * q)
+            assert torch.equal(hb[q, :2], torch.full((2,), 0.5 + q, dtype=torch.float64))
+            assert torch.isnan(hb[q, 2:]).all() and int(hc[q, 0]) == q
 
 
 @pytest.mark.parametrize("world", [2, 8])
