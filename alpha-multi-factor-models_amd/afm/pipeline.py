@@ -128,8 +128,9 @@ class PipelineConfig:
     # wave per SIMD, <= 25 blocks: the N = 8 shard) the z statistics then run on the issue slots
     # and CUs the factor kernel leaves free instead of after it.  -1: 6 on those grids, else 0.
     zstats_slabs: int = -1
-    # early_fwd -- one GPU: the analyzer's price rows and forward returns (prediction-independent,
-    # KKT:294-296) on a side stream as soon as the all_df rows exist, beside the z statistics,
+    # early_fwd -- the analyzer's price rows and forward returns (prediction-independent,
+    # KKT:294-296) on a side stream as soon as the all_df rows exist -- one GPU: beside the z
+    # statistics; N > 1: after one all-gather of the all_df row words, beside the Grams --
     # instead of at the head of the analyzer stream in the tail
     early_fwd: bool = True
     # reb_split -- N > 1: each rank runs the rebalance of its share of the dates (+ one neighbour
@@ -670,8 +671,8 @@ class Pipeline:
             one_pass = not (self.early or self.stream_z)
             if one_pass:
                 mark("factors", 1)
-            self.fwd_early = W == 1 and c.analyzer and c.early_fwd
-            if self.fwd_early:
+            self.fwd_early = c.analyzer and c.early_fwd
+            if self.fwd_early and W == 1:
                 self.side2.wait_stream(self.main)                # the all_df rows
                 with torch.cuda.stream(self.side2):
                     self._analyzer_fwd()
@@ -697,6 +698,14 @@ class Pipeline:
                                          P(full.ret1d), P(full.vbits), P(self.target),
                                          P(self.tmr)), "labels")
                     self.labels_done.record(self.side2)
+                if self.fwd_early:
+                    # the analyzer's price rows and forward returns need the whole cross-section's
+                    # all_df rows only (not the predictions): gathered now, beside the Grams, so
+                    # the analyzer's prediction-dependent chain starts right at the predict
+                    self.side2.wait_stream(self.main)            # the all_df rows (after zstats)
+                    with torch.cuda.stream(self.side2):
+                        self._gather_alldf()
+                        self._analyzer_fwd()
                 h = self.ctx.bind_stream()
             mark("xs_gram", 0)
             self._pooled_blocks(h, 0, sp.v1, mark)                  # train + valid rows
@@ -859,20 +868,37 @@ class Pipeline:
         d[:, :A] = side[:, :A]
 
     def _gather_test_planes(self):
+        """The test dates' predictions and the z-score / all_df row words of every rank's asset
+        shard -> the full-width planes (one packed all-gather; the all_df words already went
+        out with the forward returns when those run early, ``_gather_alldf``)."""
         import torch
         s0, wide, A_r = self.sp.s0, self.wide, self.A_r
-        sb = self._send_buffer("test", [((self.T - s0, wide), torch.float64, float("nan")),
-                                        ((self.nch, wide), torch.int64, 0),
-                                        ((self.nch, wide), torch.int64, 0)], self.pred_r.device)
-        pr, zb, ab = sb.parts                       # columns past A_r keep NaN / 0
+        specs = [((self.T - s0, wide), torch.float64, float("nan")),
+                 ((self.nch, wide), torch.int64, 0)]
+        with_alldf = not self.fwd_early
+        if with_alldf:
+            specs.append(((self.nch, wide), torch.int64, 0))
+        sb = self._send_buffer("test" if with_alldf else "test_noad", specs, self.pred_r.device)
+        pr, zb = sb.parts[:2]                       # columns past A_r keep NaN / 0
         if A_r > 0:
             pr[:, :A_r].copy_(self.pred_r[s0:, :A_r])
             zb[:, :A_r].copy_(self.zrows[:, :A_r])
-            ab[:, :A_r].copy_(self.alldf[:, :A_r])
-        gp, gz, ga = self.comm.all_gather_buffer(sb)
-        self._place(self.pred, gp, rows=slice(s0, self.T))
-        self._place(self.zrows_full, gz)
-        self._place(self.alldf_full, ga)
+            if with_alldf:
+                sb.parts[2][:, :A_r].copy_(self.alldf[:, :A_r])
+        got = self.comm.all_gather_buffer(sb)
+        self._place(self.pred, got[0], rows=slice(s0, self.T))
+        self._place(self.zrows_full, got[1])
+        if with_alldf:
+            self._place(self.alldf_full, got[2])
+
+    def _gather_alldf(self):
+        """Every rank's all_df row words -> the full-width ``alldf_full`` (one all-gather)."""
+        import torch
+        sb = self._send_buffer("alldf", [((self.nch, self.wide), torch.int64, 0)],
+                               self.alldf.device)
+        if self.A_r > 0:
+            sb.parts[0][:, :self.A_r].copy_(self.alldf[:, :self.A_r])
+        self._place(self.alldf_full, self.comm.all_gather_buffer(sb)[0])
 
     def _gather_rebalance(self):
         import torch

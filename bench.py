@@ -449,6 +449,8 @@ def main():
                     help="time what ONE rank of an N-GPU job computes, on one GPU (collectives "
                          "replaced by local copies, afm.sharded.EmulatedComm): a per-rank proxy, "
                          "not a result of the job")
+    ap.add_argument("--early-fwd", type=int, default=None,
+                    help="PipelineConfig.early_fwd 0/1 (A/B; default: on)")
     ap.add_argument("--reb-split", type=int, default=None,
                     help="PipelineConfig.reb_split (N > 1: 1 = rebalance dates split over the "
                          "ranks + all-gather, 0 = every rank all dates)")
@@ -510,6 +512,8 @@ def main():
         place["fm_grid"] = args.fm_grid
     if args.reb_split is not None:
         place["reb_split"] = bool(args.reb_split)
+    if args.early_fwd is not None:
+        place["early_fwd"] = bool(args.early_fwd)
     for k in ("train_end", "valid_end", "window"):
         if getattr(args, k) is not None:
             place[k] = getattr(args, k)

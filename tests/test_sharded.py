@@ -218,7 +218,8 @@ def _sharded_worker(rank, world, port, outdir, A, T, reb_split=True):
     from afm.synthetic import make_panel
     torch.cuda.set_device(0)
     grid = afm.PanelGrid.from_panel(make_panel(A, T, seed=11, tradable_p=0.9))
-    sp = ShardedPipeline(grid, Comm(), PipelineConfig(**SPLIT, reb_split=reb_split))
+    sp = ShardedPipeline(grid, Comm(), PipelineConfig(**SPLIT, reb_split=reb_split,
+                                                      early_fwd=reb_split))
     sp.step()
     sp.step()
     torch.cuda.synchronize()
@@ -253,8 +254,12 @@ def test_sharded_ranks_bit_identical_to_single(tmp_path, world, A, T, reb_split)
     8-block split (rank 7 a short one of 104 assets), runs the small-grid factor launch on its
     2-block shard (the 30-set partition PartS, code 110) with the z statistics streamed slab by
     slab behind it, owns 1/8 of the FM dates (the 8-owner all_to_all) and of the rebalance
-    dates.  (The 15-set PartC splits are covered by test_factors_gpu.py.)  reb_split False: every
-    rank runs the rebalance of every date (PipelineConfig.reb_split), no rebalance exchange."""
+    dates.  (The 15-set PartC splits are covered by test_factors_gpu.py.)  By default the
+    analyzer's forward returns run early, after an all-gather of the all_df row words beside the
+    Grams.  The reb_split False case also covers the other placements: every rank runs the
+    rebalance of every date (PipelineConfig.reb_split), no rebalance exchange, and the forward
+    returns at the head of the analyzer stream (early_fwd False: the all_df words travel with
+    the test planes)."""
     import torch
     import torch.multiprocessing as mp
     import afm
