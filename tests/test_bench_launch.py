@@ -81,3 +81,40 @@ def test_bench_self_launch_two_ranks():
     assert roofs["hbm"]["kernel"].startswith("factor_panel_kernel")
     assert roofs["mfma"]["kernel"].startswith("zgram_kernel<7,1> (pooled")
     assert roofs["mfma"]["kernel_ms"] < roofs["mfma"]["stage_ms"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_line_contract():
+    """One GPU, a small panel, with the CPU-baseline leg: the one JSON line carries every key of
+    the bench contract (metric / value / unit / n_gpus / steps / warmup / ms_per_step /
+    higher_is_better / scaling / vs_baseline / dtype / data / config) plus the roofline and
+    cpu_baseline objects, with consistent numbers."""
+    env = dict(os.environ)
+    args = [a for a in SMALL if a != "--no-cpu-baseline"]
+    r = subprocess.run([sys.executable, "-u", BENCH] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [s for s in r.stdout.splitlines() if s.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "strong" and d["dtype"] == "f64"
+    assert d["unit"] == "asset-days/s" and d["vs_baseline"] is None
+    assert "workload" in d["config"] and "model" not in d["config"]
+    # value = the whole panel's asset-days over the measured step time
+    assert d["value"] == pytest.approx(d["config"]["asset_days"] / (d["ms_per_step"] * 1e-3),
+                                       rel=1e-3)
+    rf = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rf, k
+    assert rf["bound"] in ("hbm", "mfma") and 0 < rf["frac"] < 1
+    cb = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in cb, k
+    assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] in ("port", "reference")
+
